@@ -1,0 +1,186 @@
+"""Benchmark: predicted rows/sec of the BASELINE.json headline workload.
+
+Workload (BASELINE.json configs[1]): synthetic HIGGS-shaped
+XGBoost binary:logistic model, 500 complete depth-8 trees, 28 features,
+base_score 0.5; a 1M-row float32 batch per GPU, resident in HBM when the timed
+region starts.  One step = one fused predict (traversal + sigmoid) over the
+batch.  Multi-GPU: one process per GPU (torchrun), rows sharded with no
+collective ("weak": every rank predicts its own 1M rows); value = all ranks'
+rows / max-over-ranks wall time.
+
+Also reported (rank 0):
+  roofline     -- SURVEY.md 8(d) byte model per launch: B_visit = 8 B x V + 4 B x F
+                  + 4 B out, V = node visits per row (500 x 8 = 4000), divided by
+                  the kernel's average duration measured with HIP events on the
+                  launch stream; traffic = HBM bytes from a committed rocprofv3 PMC
+                  pass (profiles/), or null.
+  cpu_baseline -- the C/OpenMP restatement of xgboost 0.82's predict loop
+                  (oracle/c/tree_port.c, kind "port": xgboost is not installed)
+                  timed on this host on a bounded sample of the same rows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_TREES, DEPTH, N_FEAT, ROWS = 500, 8, 28, 1_000_000
+HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md)
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--rows", type=int, default=ROWS)
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="target CPU work for the cpu_baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
+    return p.parse_args()
+
+
+def build_model():
+    from kfserving_amd.formats.xgboost_format import (forest_from_raw_trees,
+                                                      synthetic_complete_trees)
+    trees, ti = synthetic_complete_trees(N_TREES, DEPTH, N_FEAT, seed=0)
+    # xgboost 0.82 stores base_score in margin space: ProbToMargin(0.5) = 0
+    forest = forest_from_raw_trees(trees, ti, N_FEAT, 0, 0.0, "binary:logistic")
+    return trees, ti, forest
+
+
+def shard_rows(total_rows: int, rank: int, world: int):
+    """Weak scaling: every rank owns a full batch of `total_rows` rows with its own seed."""
+    return total_rows, 1000 + rank
+
+
+def cpu_baseline(trees, ti, X_host, target_s):
+    from oracle import port
+    n_thr = port.num_threads()
+    probe = min(20_000, X_host.shape[0])
+    t0 = time.perf_counter()
+    port.xgb_predict(trees, ti, 1, 0.0, N_FEAT, X_host[:probe], sigmoid=True)
+    rate = probe / max(time.perf_counter() - t0, 1e-9)
+    n = int(min(X_host.shape[0], max(probe, rate * target_s)))
+    t0 = time.perf_counter()
+    port.xgb_predict(trees, ti, 1, 0.0, N_FEAT, X_host[:n], sigmoid=True)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "rows/s", "cores": n_thr, "kind": "port",
+            "sample": f"{n} rows of the same 1M x 28 batch, oracle/c/tree_port.c "
+                      f"(xgboost 0.82 predict loop restated, OpenMP {n_thr} threads), "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local_rank)
+
+    from kfserving_amd.engine import DeviceForest
+    from kfserving_amd.forest import OUT_PREDICT, TI_F32
+
+    trees, ti, forest = build_model()
+    dev = DeviceForest(forest, devices=[local_rank])
+    info = dev.info()
+    rows, seed = shard_rows(args.rows, rank, world)
+    X_host = np.random.default_rng(seed).standard_normal((rows, N_FEAT), dtype=np.float32)
+    X = torch.from_numpy(X_host).to(f"cuda:{local_rank}")
+    out = torch.empty(rows, dtype=torch.float32, device=f"cuda:{local_rank}")
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    def step():
+        dev.predict_device(X.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
+                           out.data_ptr(), rows, slot=0, stream=sh)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    total_rows = rows * world * args.steps
+    value = total_rows / wall
+
+    if rank == 0:
+        visits = N_TREES * DEPTH                     # complete trees: every row visits D nodes
+        b_visit = 8 * visits + 4 * N_FEAT + 4        # SURVEY.md 8(d) B_visit
+        achieved = b_visit * rows / (kernel_ms * 1e-3)
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                with open(args.traffic_json) as fh:
+                    pmc = json.load(fh)
+                if pmc.get("rows") == rows and pmc.get("workload") == "c2":
+                    traffic = pmc.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        roofline = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                    "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
+                    "bytes_per_row_visit_model": b_visit,
+                    "compulsory_GBps": (4 * N_FEAT + 4) * rows / (kernel_ms * 1e-3) / 1e9,
+                    "kernel_ms": kernel_ms}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(trees, ti, X_host, args.cpu_seconds)
+        line = {
+            "metric": "predicted rows/sec (500-tree XGB, 28 feat)",
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: X ~ N(0,1) float32, seeded; random 500 x depth-8 XGBoost "
+                    "binary:logistic trees (SURVEY.md 8(d) C2)",
+            "config": {"workload": "C2 synthetic HIGGS-shaped XGBoost binary: 28 features, "
+                                   "500 trees depth 8, 1M-row batch per GPU",
+                       "rows_per_gpu": rows, "trees": N_TREES, "depth": DEPTH,
+                       "features": N_FEAT, "layout": "heap" if info["layout"] == 0 else
+                       "explicit", "parallelism": f"rows sharded x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,194 @@
+/*
+ * treeinfer.h — C ABI of the MI355X batched tree-ensemble inference engine
+ * (libtreeinfer.so, built from kfserving_amd/csrc/).
+ *
+ * This is the drop-in boundary for the KFServing tree-predict hot path.
+ * The reference never calls a GPU: its three tree plugins hand a batch to a
+ * third-party CPU library through that library's own ctypes binding:
+ *
+ *   python/xgbserver/xgbserver/model.py:46-47
+ *       xgb.DMatrix(request["instances"]) ; self._booster.predict(dmatrix)
+ *       -> upstream xgboost 0.82 C API  XGBoosterPredict(BoosterHandle,
+ *          DMatrixHandle, int option_mask, unsigned ntree_limit,
+ *          bst_ulong* out_len, const float** out_result)
+ *   python/lgbserver/lgbserver/model.py:46-51
+ *       self._booster.predict(pd.concat(dfs))
+ *       -> upstream lightgbm 2.3.1 C API  LGBM_BoosterPredictForMat(handle,
+ *          const void* data, int data_type, int32 nrow, int32 ncol,
+ *          int is_row_major, int predict_type, int num_iteration,
+ *          const char* parameter, int64* out_len, double* out_result)
+ *   python/sklearnserver/sklearnserver/model.py:46-51
+ *       self._model.predict(np.array(instances))
+ *       -> sklearn ForestRegressor/ForestClassifier.predict (Cython)
+ *
+ * and each plugin's load() builds the library handle:
+ *   python/xgbserver/xgbserver/model.py:35-41   xgb.Booster(model_file=...)
+ *   python/lgbserver/lgbserver/model.py:36-42   lgb.Booster(model_file=...)
+ *   python/sklearnserver/sklearnserver/model.py:32-41  joblib.load(...)
+ *
+ * The entry points below replace those library calls one for one, keeping
+ * the conventions of the libraries' own C APIs: int return (0 = success,
+ * negative = error), a thread-local last-error string, an opaque handle
+ * created from the model and released by the caller, caller-owned output
+ * buffers.  Host code (the kfserving_amd package) parses the model files itself
+ * into the canonical structure-of-arrays forest described by
+ * ti_forest_desc and binds these symbols with ctypes.
+ *
+ * Canonical split semantics (one rule for all three libraries):
+ *   at internal node n with feature f = feature[n], input value x = X[row,f]:
+ *     LightGBM inputs only (desc.lgb_zero_map): |x| <= 1e-35f  ->  x = 0
+ *     if x is NaN:            go left iff flags[n] & TI_NODE_NAN_LEFT
+ *     else if x == 0 and (flags[n] & TI_NODE_ZERO_FLIP):
+ *                             go left iff !(0 <= threshold[n])
+ *     else:                   go left iff x <= threshold[n]
+ *   The host encodes each library's rule into threshold/flags:
+ *     XGBoost  (x < t, f32)  : threshold = nextafterf(t, -inf) (NaN if t=-inf),
+ *                              NAN_LEFT = default_left
+ *     LightGBM (x <= t, f64) : threshold = t, NAN_LEFT / ZERO_FLIP from the
+ *                              node's missing type (None / Zero / NaN)
+ *     sklearn  (f32 x <= f64 t): threshold = t, NAN_LEFT = missing_go_to_left
+ *   For float32 inputs the library compares against round_down_f32(threshold),
+ *   which is exact for every float32 x; float64 inputs compare in float64.
+ */
+#ifndef TREEINFER_H_
+#define TREEINFER_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TI_ABI_VERSION 1
+
+/* return codes */
+#define TI_OK               0
+#define TI_ERR_INVALID     -1   /* bad argument / malformed forest        */
+#define TI_ERR_DEVICE      -2   /* HIP runtime error                      */
+#define TI_ERR_NOMEM       -3   /* host or device allocation failed       */
+#define TI_ERR_UNSUPPORTED -4   /* forest shape the engine cannot run     */
+
+/* element types */
+#define TI_F32 0
+#define TI_F64 1
+#define TI_I32 2
+
+/* node flag bits (ti_forest_desc.flags) */
+#define TI_NODE_NAN_LEFT   0x01  /* NaN input goes left                    */
+#define TI_NODE_ZERO_FLIP  0x02  /* x == 0 takes the opposite of (0 <= t)  */
+
+/* output transforms applied after accumulation (ti_forest_desc.transform) */
+#define TI_TRANSFORM_IDENTITY    0
+#define TI_TRANSFORM_SIGMOID     1  /* 1/(1+exp(-param*x)), per output       */
+#define TI_TRANSFORM_SOFTMAX     2  /* over the n_groups outputs             */
+#define TI_TRANSFORM_ARGMAX      3  /* index of the first maximum, as value  */
+#define TI_TRANSFORM_HINGE       4  /* x > 0 ? 1 : 0                         */
+#define TI_TRANSFORM_EXP         5  /* exp(x)                                */
+#define TI_TRANSFORM_SIGNSQUARE  6  /* sign(x) * x * x (LightGBM sqrt)       */
+#define TI_TRANSFORM_LOG1PEXP    7  /* log(1 + exp(x)) (LightGBM xentlambda) */
+
+/* what ti_predict writes */
+#define TI_OUTPUT_MARGIN   0  /* raw score (after base/average), [rows, K]     */
+#define TI_OUTPUT_PREDICT  1  /* transformed score, [rows, K] or [rows]       */
+#define TI_OUTPUT_LEAF     2  /* library leaf id per tree (int32), [rows, T]   */
+
+/*
+ * Canonical forest: host structure-of-arrays over the nodes of all trees,
+ * trees concatenated.  Node indices in left/right are tree-local.
+ * All pointers are read during ti_forest_create only.
+ */
+typedef struct ti_forest_desc {
+  int32_t abi_version;        /* = TI_ABI_VERSION                                   */
+  int32_t n_trees;            /* T                                                  */
+  int32_t n_features;         /* F: columns the forest may read                     */
+  int32_t n_groups;           /* K: outputs per row                                 */
+  int32_t leaf_width;         /* 1: scalar leaf added to output tree_group[t];      */
+                              /* K: vector leaf added to all K outputs              */
+  int32_t accum_dtype;        /* TI_F32 (XGBoost) or TI_F64 (LightGBM, sklearn)     */
+  int32_t base_first;         /* 1: acc starts at base_margin (xgboost>=1, lgb, sk) */
+                              /* 0: acc starts at 0, margin = base + acc (xgb 0.82) */
+  int32_t lgb_zero_map;       /* 1: |x| <= 1e-35f reads as 0 (LightGBM predictor)   */
+  int64_t n_nodes;            /* N                                                  */
+  const int64_t* tree_offset; /* [T+1] first node of each tree                      */
+  const int32_t* tree_group;  /* [T]   output group of each tree (leaf_width == 1)  */
+  const int32_t* feature;     /* [N]   split feature, -1 for a leaf                 */
+  const double*  threshold;   /* [N]   canonical threshold: left iff x <= t         */
+  const uint8_t* flags;       /* [N]   TI_NODE_* bits                               */
+  const int32_t* left;        /* [N]   left child (tree-local), -1 for a leaf       */
+  const int32_t* right;       /* [N]   right child (tree-local), -1 for a leaf      */
+  const int32_t* leaf_id;     /* [N]   id reported by TI_OUTPUT_LEAF for a leaf     */
+  const double*  leaf_value;  /* [N * leaf_width] leaf payload (read for leaves)    */
+  const double*  base_margin; /* [K]                                                */
+  double  average_divisor;    /* margin /= divisor after accumulation (1 = none)    */
+  int32_t transform;          /* TI_TRANSFORM_*                                     */
+  int32_t reserved0;
+  double  transform_param;    /* sigmoid scale                                      */
+} ti_forest_desc;
+
+typedef struct ti_forest ti_forest;   /* opaque, owns device memory */
+
+/* Layout the engine chose for a forest (diagnostics, bench byte models). */
+typedef struct ti_forest_info {
+  int32_t layout;             /* 0 = heap (complete, LDS-staged), 1 = explicit nodes */
+  int32_t depth;              /* heap depth D, or max depth for explicit             */
+  int32_t n_trees;
+  int32_t n_groups;
+  int32_t n_features;
+  int32_t n_devices;
+  int64_t device_bytes;       /* forest bytes resident per device                   */
+  int64_t tree_stride_bytes;  /* heap layout: bytes per staged tree                 */
+} ti_forest_info;
+
+/* Upload the forest to each listed device (HIP device ordinals).  HIP is
+ * initialised here, not at library load, so a process may fork before it.
+ * Replaces: xgb.Booster(model_file=...) (xgbserver/model.py:38-39),
+ *           lgb.Booster(model_file=...) (lgbserver/model.py:39-40),
+ *           joblib.load(...)            (sklearnserver/model.py:38). */
+int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices,
+                     int32_t n_devices, ti_forest** out);
+
+/* Release device memory and the handle (XGBoosterFree / LGBM_BoosterFree). */
+int ti_forest_destroy(ti_forest* forest);
+
+int ti_forest_get_info(const ti_forest* forest, ti_forest_info* info);
+
+/* Number of elements and element type ti_predict writes for n_rows rows. */
+int ti_output_shape(const ti_forest* forest, int32_t output_kind, int64_t n_rows,
+                    int64_t* out_len, int32_t* out_dtype);
+
+/* Host-buffer predict.  X: [n_rows, n_cols] row-major with row_stride
+ * elements between rows, element type x_dtype (TI_F32/TI_F64); out: caller-
+ * owned host buffer of out_len elements (see ti_output_shape).  Rows are
+ * sharded in contiguous blocks across the forest's devices; the call blocks
+ * until the result is in `out`.  Thread-safe per handle.
+ * Replaces: XGBoosterPredict (xgbserver/model.py:46-47),
+ *           LGBM_BoosterPredictForMat (lgbserver/model.py:51),
+ *           ForestRegressor/Classifier.predict (sklearnserver/model.py:50). */
+int ti_predict(ti_forest* forest, const void* X, int32_t x_dtype, int64_t n_rows,
+               int32_t n_cols, int64_t row_stride, int32_t output_kind,
+               void* out, int64_t out_len);
+
+/* Device-resident predict on one of the forest's devices (device_slot indexes
+ * the devices passed to ti_forest_create).  X and out are device pointers on
+ * that device; the kernels are enqueued on `hip_stream` (a hipStream_t, NULL =
+ * the default stream) and the call returns without synchronising. */
+int ti_predict_device(ti_forest* forest, int32_t device_slot, const void* X,
+                      int32_t x_dtype, int64_t n_rows, int32_t n_cols,
+                      int64_t row_stride, int32_t output_kind, void* out,
+                      int64_t out_len, void* hip_stream);
+
+/* Thread-local message for the last failing call on this thread
+ * (XGBGetLastError / LGBM_GetLastError). */
+const char* ti_last_error(void);
+
+/* HIP device count visible to this process (initialises HIP). */
+int ti_device_count(int32_t* count);
+
+/* TI_ABI_VERSION of the loaded library. */
+int32_t ti_abi_version(void);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* TREEINFER_H_ */

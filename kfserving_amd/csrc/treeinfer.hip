@@ -1,0 +1,674 @@
+// treeinfer.hip — libtreeinfer.so: C ABI (include/treeinfer.h) over the
+// gfx950 kernels in treeinfer_kernels.h.
+//
+// Host responsibilities:
+//   * validate the canonical SoA forest handed over by the Python loaders
+//     (kfserving_amd/formats/*), which replaces the library handles built in
+//     xgbserver/model.py:38-39, lgbserver/model.py:39-40,
+//     sklearnserver/model.py:38;
+//   * choose a device layout (heap = complete trees staged in LDS, or
+//     explicit nodes) and upload one replica per device;
+//   * ti_predict: shard rows in contiguous blocks over the devices (one host
+//     thread per device, one stream each), H2D -> one fused kernel -> D2H.
+//     This replaces XGBoosterPredict / LGBM_BoosterPredictForMat /
+//     Forest*.predict at xgbserver/model.py:46-47, lgbserver/model.py:51,
+//     sklearnserver/model.py:50.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "treeinfer.h"
+#include "treeinfer_kernels.h"
+
+using ti::ExpNode;
+using ti::HeapNode;
+using ti::KArgs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define TI_HIP(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(TI_ERR_DEVICE, std::string(#expr) + " failed: " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kMaxHeapDepth = 8;              // deeper forests use the explicit layout
+constexpr size_t kLdsPerCu = 160 * 1024;      // gfx950
+constexpr size_t kLdsTwoPerCu = 80 * 1024;    // budget for 2 workgroups / CU
+constexpr size_t kFeatLdsMax = 64 * 1024;     // feature image budget per workgroup
+
+size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+float round_down_f32(double t) {
+  if (std::isnan(t)) return NAN;
+  float f = static_cast<float>(t);
+  if (static_cast<double>(f) > t) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+
+uint32_t make_meta(int32_t feature, uint8_t flags) {
+  uint32_t m = static_cast<uint32_t>(feature) & ti::kMetaFeatMask;
+  if (flags & TI_NODE_NAN_LEFT) m |= ti::kMetaNanLeft;
+  if (flags & TI_NODE_ZERO_FLIP) m |= ti::kMetaZeroFlip;
+  return m;
+}
+
+// padded heap node below a shallow leaf: always left (x <= +inf, NaN left)
+constexpr uint32_t kPadMeta = ti::kMetaNanLeft;
+
+struct DeviceForest {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  // heap layout: one record per tree, float32-input and float64-input flavours
+  unsigned char* heap32 = nullptr;
+  unsigned char* heap64 = nullptr;
+  int32_t* heap_leaf_ids = nullptr;
+  // explicit layout
+  ExpNode* nodes = nullptr;
+  double* thr64 = nullptr;
+  int64_t* node_base = nullptr;
+  int32_t* root = nullptr;
+  int64_t* leaf_base = nullptr;
+  void* leaves = nullptr;
+  int32_t* exp_leaf_ids = nullptr;
+  int32_t* tree_group = nullptr;
+  // ti_predict scratch
+  void* x_buf = nullptr;
+  size_t x_cap = 0;
+  void* out_buf = nullptr;
+  size_t out_cap = 0;
+  int64_t bytes = 0;
+  std::mutex mu;
+};
+
+}  // namespace
+
+struct ti_forest {
+  int32_t T = 0, F = 0, K = 1, LW = 1, accum = TI_F32, base_first = 1, lgb_zero_map = 0;
+  int32_t zero_rule = 0, transform = TI_TRANSFORM_IDENTITY;
+  double tparam = 1.0, divisor = 1.0;
+  double base[ti::kMaxGroups] = {0};
+  int32_t layout = 0;   // 0 heap, 1 explicit
+  int32_t depth = 0;
+  int64_t stride32 = 0, stride64 = 0;
+  // host images (kept until upload)
+  std::vector<unsigned char> h_heap32, h_heap64;
+  std::vector<int32_t> h_heap_leaf_ids;
+  std::vector<ExpNode> h_nodes;
+  std::vector<double> h_thr64;
+  std::vector<int64_t> h_node_base, h_leaf_base;
+  std::vector<int32_t> h_root, h_exp_leaf_ids, h_group;
+  std::vector<unsigned char> h_leaves;   // ACC-typed
+  std::vector<std::unique_ptr<DeviceForest>> devs;
+};
+
+namespace {
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& src, int64_t* bytes) {
+  *dst = nullptr;
+  if (src.empty()) return TI_OK;
+  const size_t n = src.size() * sizeof(T);
+  TI_HIP(hipMalloc(reinterpret_cast<void**>(dst), n));
+  TI_HIP(hipMemcpy(*dst, src.data(), n, hipMemcpyHostToDevice));
+  *bytes += static_cast<int64_t>(n);
+  return TI_OK;
+}
+
+void free_device(DeviceForest& d) {
+  if (d.device < 0) return;
+  (void)hipSetDevice(d.device);
+  void* ptrs[] = {d.heap32, d.heap64, d.heap_leaf_ids, d.nodes, d.thr64, d.node_base, d.root,
+                  d.leaf_base, d.leaves, d.exp_leaf_ids, d.tree_group, d.x_buf, d.out_buf};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+  d.heap32 = d.heap64 = nullptr;
+  d.heap_leaf_ids = d.root = d.exp_leaf_ids = d.tree_group = nullptr;
+  d.nodes = nullptr;
+  d.thr64 = nullptr;
+  d.node_base = d.leaf_base = nullptr;
+  d.leaves = d.x_buf = d.out_buf = nullptr;
+  d.x_cap = d.out_cap = 0;
+  d.stream = nullptr;
+  d.device = -1;
+}
+
+// -------------------------------------------------------------- validation
+int validate(const ti_forest_desc* d, std::vector<int>* depth_out) {
+  if (!d) return fail(TI_ERR_INVALID, "null forest descriptor");
+  if (d->abi_version != TI_ABI_VERSION)
+    return fail(TI_ERR_INVALID, "abi_version mismatch: got " + std::to_string(d->abi_version));
+  if (d->n_trees <= 0) return fail(TI_ERR_INVALID, "n_trees must be > 0");
+  if (d->n_features <= 0 || d->n_features > (1 << 24))
+    return fail(TI_ERR_INVALID, "n_features out of range");
+  if (d->n_groups <= 0) return fail(TI_ERR_INVALID, "n_groups must be > 0");
+  if (d->n_groups > ti::kMaxGroups)
+    return fail(TI_ERR_UNSUPPORTED, "n_groups > 16 is not supported by this build");
+  if (d->leaf_width != 1 && d->leaf_width != d->n_groups)
+    return fail(TI_ERR_INVALID, "leaf_width must be 1 or n_groups");
+  if (d->accum_dtype != TI_F32 && d->accum_dtype != TI_F64)
+    return fail(TI_ERR_INVALID, "accum_dtype must be TI_F32 or TI_F64");
+  if (d->transform < TI_TRANSFORM_IDENTITY || d->transform > TI_TRANSFORM_LOG1PEXP)
+    return fail(TI_ERR_INVALID, "unknown transform");
+  if (!(d->average_divisor > 0.0)) return fail(TI_ERR_INVALID, "average_divisor must be > 0");
+  if (!d->tree_offset || !d->feature || !d->threshold || !d->flags || !d->left || !d->right ||
+      !d->leaf_id || !d->leaf_value || !d->base_margin)
+    return fail(TI_ERR_INVALID, "null array in forest descriptor");
+  if (d->leaf_width == 1 && !d->tree_group) return fail(TI_ERR_INVALID, "null tree_group");
+  if (d->tree_offset[0] != 0 || d->tree_offset[d->n_trees] != d->n_nodes)
+    return fail(TI_ERR_INVALID, "tree_offset must start at 0 and end at n_nodes");
+  depth_out->assign(d->n_trees, 0);
+  std::vector<int> stack_node, stack_depth;
+  for (int t = 0; t < d->n_trees; ++t) {
+    const int64_t b = d->tree_offset[t], e = d->tree_offset[t + 1];
+    if (e <= b) return fail(TI_ERR_INVALID, "tree " + std::to_string(t) + " has no nodes");
+    if (e - b > (int64_t(1) << 30)) return fail(TI_ERR_INVALID, "tree too large");
+    const int32_t n = static_cast<int32_t>(e - b);
+    if (d->leaf_width == 1 && (d->tree_group[t] < 0 || d->tree_group[t] >= d->n_groups))
+      return fail(TI_ERR_INVALID, "tree_group out of range in tree " + std::to_string(t));
+    int max_depth = 0;
+    int64_t visited = 0;
+    stack_node.assign(1, 0);
+    stack_depth.assign(1, 0);
+    while (!stack_node.empty()) {
+      const int v = stack_node.back(), dep = stack_depth.back();
+      stack_node.pop_back();
+      stack_depth.pop_back();
+      if (++visited > n) return fail(TI_ERR_INVALID, "cycle in tree " + std::to_string(t));
+      const int64_t g = b + v;
+      if (d->feature[g] < 0) {
+        max_depth = std::max(max_depth, dep);
+        continue;
+      }
+      if (d->feature[g] >= d->n_features)
+        return fail(TI_ERR_INVALID, "split feature >= n_features in tree " + std::to_string(t));
+      const int32_t l = d->left[g], r = d->right[g];
+      if (l < 0 || l >= n || r < 0 || r >= n)
+        return fail(TI_ERR_INVALID, "child index out of range in tree " + std::to_string(t));
+      if (dep + 1 > 64) return fail(TI_ERR_UNSUPPORTED, "tree deeper than 64");
+      stack_node.push_back(l);
+      stack_depth.push_back(dep + 1);
+      stack_node.push_back(r);
+      stack_depth.push_back(dep + 1);
+    }
+    (*depth_out)[t] = max_depth;
+  }
+  return TI_OK;
+}
+
+// ------------------------------------------------------------ heap packing
+template <typename XT, typename ACC>
+void pack_heap(const ti_forest_desc* d, int D, int64_t stride, std::vector<unsigned char>* img,
+               std::vector<int32_t>* leaf_ids) {
+  using Node = HeapNode<XT>;
+  const int NI = (1 << D) - 1, NL = 1 << D, LW = d->leaf_width;
+  img->assign(static_cast<size_t>(stride) * d->n_trees, 0);
+  if (leaf_ids) leaf_ids->assign(static_cast<size_t>(NL) * d->n_trees, 0);
+  struct Item { int32_t node; int32_t heap; int32_t level; };
+  std::vector<Item> st;
+  for (int t = 0; t < d->n_trees; ++t) {
+    unsigned char* rec = img->data() + static_cast<size_t>(stride) * t;
+    Node* nodes = reinterpret_cast<Node*>(rec);
+    ACC* leaves = reinterpret_cast<ACC*>(rec + sizeof(Node) * NI);
+    const int64_t b = d->tree_offset[t];
+    st.assign(1, Item{0, 0, 0});
+    while (!st.empty()) {
+      const Item it = st.back();
+      st.pop_back();
+      const int64_t g = b + it.node;
+      if (it.level == D) {   // leaf slot
+        const int slot = it.heap - NI;
+        for (int k = 0; k < LW; ++k)
+          leaves[static_cast<size_t>(slot) * LW + k] = static_cast<ACC>(d->leaf_value[g * LW + k]);
+        if (leaf_ids) (*leaf_ids)[static_cast<size_t>(t) * NL + slot] = d->leaf_id[g];
+        continue;
+      }
+      Node nd{};
+      if (d->feature[g] < 0) {   // shallow leaf: pad with always-left nodes
+        nd.thr = static_cast<decltype(nd.thr)>(INFINITY);
+        nd.meta = kPadMeta;
+        nodes[it.heap] = nd;
+        st.push_back(Item{it.node, 2 * it.heap + 1, it.level + 1});
+        st.push_back(Item{it.node, 2 * it.heap + 2, it.level + 1});
+      } else {
+        if (sizeof(XT) == 4)
+          nd.thr = static_cast<decltype(nd.thr)>(round_down_f32(d->threshold[g]));
+        else
+          nd.thr = static_cast<decltype(nd.thr)>(d->threshold[g]);
+        nd.meta = make_meta(d->feature[g], d->flags[g]);
+        nodes[it.heap] = nd;
+        st.push_back(Item{d->left[g], 2 * it.heap + 1, it.level + 1});
+        st.push_back(Item{d->right[g], 2 * it.heap + 2, it.level + 1});
+      }
+    }
+  }
+}
+
+// -------------------------------------------------------- explicit packing
+template <typename ACC>
+void pack_explicit(const ti_forest_desc* d, ti_forest* f) {
+  const int LW = d->leaf_width;
+  f->h_nodes.clear();
+  f->h_thr64.clear();
+  f->h_node_base.assign(d->n_trees, 0);
+  f->h_leaf_base.assign(d->n_trees, 0);
+  f->h_root.assign(d->n_trees, 0);
+  f->h_exp_leaf_ids.clear();
+  std::vector<ACC> leaves;
+  std::vector<int32_t> remap;
+  std::vector<int32_t> queue;
+  for (int t = 0; t < d->n_trees; ++t) {
+    const int64_t b = d->tree_offset[t];
+    const int32_t n = static_cast<int32_t>(d->tree_offset[t + 1] - b);
+    remap.assign(n, 0);
+    const int64_t nb = static_cast<int64_t>(f->h_nodes.size());
+    const int64_t lb = static_cast<int64_t>(f->h_exp_leaf_ids.size());
+    f->h_node_base[t] = nb;
+    f->h_leaf_base[t] = lb;
+    // breadth-first numbering: the top levels of a tree share cache lines
+    queue.assign(1, 0);
+    int32_t n_int = 0, n_leaf = 0;
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+      const int32_t v = queue[qi];
+      const int64_t g = b + v;
+      if (d->feature[g] < 0) {
+        remap[v] = ~n_leaf++;
+        f->h_exp_leaf_ids.push_back(d->leaf_id[g]);
+        for (int k = 0; k < LW; ++k) leaves.push_back(static_cast<ACC>(d->leaf_value[g * LW + k]));
+      } else {
+        remap[v] = n_int++;
+        queue.push_back(d->left[g]);
+        queue.push_back(d->right[g]);
+      }
+    }
+    f->h_nodes.resize(nb + n_int);
+    f->h_thr64.resize(nb + n_int);
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+      const int32_t v = queue[qi];
+      const int64_t g = b + v;
+      if (d->feature[g] < 0) continue;
+      ExpNode e;
+      e.thr = round_down_f32(d->threshold[g]);
+      e.meta = make_meta(d->feature[g], d->flags[g]);
+      e.left = remap[d->left[g]];
+      e.right = remap[d->right[g]];
+      f->h_nodes[nb + remap[v]] = e;
+      f->h_thr64[nb + remap[v]] = d->threshold[g];
+    }
+    f->h_root[t] = remap[0];
+  }
+  f->h_leaves.resize(leaves.size() * sizeof(ACC));
+  if (!leaves.empty()) std::memcpy(f->h_leaves.data(), leaves.data(), f->h_leaves.size());
+}
+
+int upload_device(ti_forest* f, DeviceForest& d, int device) {
+  d.device = device;
+  TI_HIP(hipSetDevice(device));
+  TI_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  int rc;
+  if ((rc = upload(&d.tree_group, f->h_group, &d.bytes))) return rc;
+  if (f->layout == 0) {
+    if ((rc = upload(&d.heap32, f->h_heap32, &d.bytes))) return rc;
+    if ((rc = upload(&d.heap64, f->h_heap64, &d.bytes))) return rc;
+    if ((rc = upload(&d.heap_leaf_ids, f->h_heap_leaf_ids, &d.bytes))) return rc;
+  } else {
+    if ((rc = upload(&d.nodes, f->h_nodes, &d.bytes))) return rc;
+    if ((rc = upload(&d.thr64, f->h_thr64, &d.bytes))) return rc;
+    if ((rc = upload(&d.node_base, f->h_node_base, &d.bytes))) return rc;
+    if ((rc = upload(&d.root, f->h_root, &d.bytes))) return rc;
+    if ((rc = upload(&d.leaf_base, f->h_leaf_base, &d.bytes))) return rc;
+    unsigned char* lv = nullptr;
+    if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
+    d.leaves = lv;
+    if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
+  }
+  return TI_OK;
+}
+
+// ----------------------------------------------------------------- launch
+using KernelFn = void (*)(KArgs);
+
+template <typename XT, typename ACC, int KMAX, bool FL>
+KernelFn pick_kernel(int layout) {
+  if (layout == 0) return ti::heap_predict_kernel<XT, ACC, KMAX, FL>;
+  return ti::explicit_predict_kernel<XT, ACC, KMAX, FL>;
+}
+
+template <typename XT, typename ACC, int KMAX>
+KernelFn pick_kernel_fl(int layout, bool fl) {
+  return fl ? pick_kernel<XT, ACC, KMAX, true>(layout) : pick_kernel<XT, ACC, KMAX, false>(layout);
+}
+
+template <typename XT, typename ACC>
+KernelFn pick_kernel_k(int layout, int K, bool fl) {
+  if (K == 1) return pick_kernel_fl<XT, ACC, 1>(layout, fl);
+  if (K <= 4) return pick_kernel_fl<XT, ACC, 4>(layout, fl);
+  return pick_kernel_fl<XT, ACC, 16>(layout, fl);
+}
+
+KernelFn select_kernel(int layout, int xdt, int accum, int K, bool fl) {
+  if (xdt == TI_F32 && accum == TI_F32) return pick_kernel_k<float, float>(layout, K, fl);
+  if (xdt == TI_F32 && accum == TI_F64) return pick_kernel_k<float, double>(layout, K, fl);
+  if (xdt == TI_F64 && accum == TI_F64) return pick_kernel_k<double, double>(layout, K, fl);
+  return pick_kernel_k<double, float>(layout, K, fl);
+}
+
+std::mutex g_attr_mu;
+std::set<std::pair<int, const void*>> g_attr_done;
+
+int ensure_lds_attr(int device, KernelFn fn, size_t lds) {
+  if (lds <= 64 * 1024) return TI_OK;
+  std::lock_guard<std::mutex> lk(g_attr_mu);
+  auto key = std::make_pair(device, reinterpret_cast<const void*>(fn));
+  if (g_attr_done.count(key)) return TI_OK;
+  TI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsPerCu)));
+  g_attr_done.insert(key);
+  return TI_OK;
+}
+
+int64_t output_width(const ti_forest* f, int kind) {
+  if (kind == TI_OUTPUT_LEAF) return f->T;
+  if (kind == TI_OUTPUT_PREDICT && f->transform == TI_TRANSFORM_ARGMAX) return 1;
+  return f->K;
+}
+
+int output_dtype(const ti_forest* f, int kind) {
+  if (kind == TI_OUTPUT_LEAF) return TI_I32;
+  return f->accum;
+}
+
+size_t dtype_size(int dt) { return dt == TI_F64 ? 8 : 4; }
+
+int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, int32_t cols,
+           int64_t stride, int kind, void* out, hipStream_t stream) {
+  if (rows <= 0) return TI_OK;
+  const size_t xs = dtype_size(xdt);
+  // block size = rows per tile; keep the [F][R] feature image <= 64 KiB
+  int R = 256;
+  while (R > 64 && static_cast<size_t>(f->F) * R * xs > kFeatLdsMax) R >>= 1;
+  bool feat_lds = static_cast<size_t>(f->F) * R * xs <= kFeatLdsMax;
+  if (!feat_lds) R = 256;
+  const size_t feat_bytes = feat_lds ? align16(static_cast<size_t>(f->F) * R * xs) : 0;
+
+  KArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.X = X;
+  a.n_rows = rows;
+  a.row_stride = stride;
+  a.n_cols = cols;
+  a.n_features = f->F;
+  a.n_trees = f->T;
+  a.n_groups = f->K;
+  a.leaf_width = f->LW;
+  a.kind = kind;
+  a.transform = f->transform;
+  a.base_first = f->base_first;
+  a.lgb_zero_map = f->lgb_zero_map;
+  a.zero_rule = f->zero_rule;
+  a.divide = f->divisor != 1.0;
+  a.transform_param = f->tparam;
+  a.average_divisor = f->divisor;
+  for (int k = 0; k < ti::kMaxGroups; ++k) a.base[k] = f->base[k];
+  a.tree_group = d.tree_group;
+  a.out = out;
+
+  size_t lds = feat_bytes;
+  if (f->layout == 0) {
+    const int64_t stride_b = xdt == TI_F64 ? f->stride64 : f->stride32;
+    a.trees = xdt == TI_F64 ? d.heap64 : d.heap32;
+    a.tree_stride = stride_b;
+    a.heap_leaf_ids = d.heap_leaf_ids;
+    a.depth = f->depth;
+    size_t budget = kLdsTwoPerCu > feat_bytes ? kLdsTwoPerCu - feat_bytes : 0;
+    int64_t S = static_cast<int64_t>(budget / stride_b);
+    if (S < 4) S = static_cast<int64_t>((kLdsPerCu - feat_bytes) / stride_b);
+    if (S < 1) return fail(TI_ERR_UNSUPPORTED, "heap tree record does not fit in LDS");
+    S = std::min<int64_t>(S, f->T);
+    a.stage_trees = static_cast<int32_t>(S);
+    lds = feat_bytes + static_cast<size_t>(S * stride_b);
+  } else {
+    a.nodes = d.nodes;
+    a.thr64 = d.thr64;
+    a.node_base = d.node_base;
+    a.root = d.root;
+    a.leaf_base = d.leaf_base;
+    a.leaves = d.leaves;
+    a.exp_leaf_ids = d.exp_leaf_ids;
+  }
+  if (lds == 0) lds = 16;
+  KernelFn fn = select_kernel(f->layout, xdt, f->accum, f->K, feat_lds);
+  int rc = ensure_lds_attr(d.device, fn, lds);
+  if (rc) return rc;
+  const int64_t grid = (rows + R - 1) / R;
+  if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+  TI_HIP(hipGetLastError());
+  return TI_OK;
+}
+
+int grow(void** buf, size_t* cap, size_t need) {
+  if (need <= *cap) return TI_OK;
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  size_t n = std::max(need, static_cast<size_t>(1) << 20);
+  TI_HIP(hipMalloc(buf, n));
+  *cap = n;
+  return TI_OK;
+}
+
+int predict_shard(ti_forest* f, DeviceForest& d, const unsigned char* X, int xdt, int64_t rows,
+                  int32_t cols, int64_t stride, int kind, unsigned char* out) {
+  std::lock_guard<std::mutex> lk(d.mu);
+  TI_HIP(hipSetDevice(d.device));
+  const size_t xs = dtype_size(xdt);
+  const size_t x_elems = static_cast<size_t>((rows - 1) * stride + cols);
+  const size_t out_bytes = static_cast<size_t>(rows * output_width(f, kind)) *
+                           dtype_size(output_dtype(f, kind));
+  int rc;
+  if ((rc = grow(&d.x_buf, &d.x_cap, x_elems * xs))) return rc;
+  if ((rc = grow(&d.out_buf, &d.out_cap, out_bytes))) return rc;
+  TI_HIP(hipMemcpyAsync(d.x_buf, X, x_elems * xs, hipMemcpyHostToDevice, d.stream));
+  if ((rc = launch(f, d, d.x_buf, xdt, rows, cols, stride, kind, d.out_buf, d.stream))) return rc;
+  TI_HIP(hipMemcpyAsync(out, d.out_buf, out_bytes, hipMemcpyDeviceToHost, d.stream));
+  TI_HIP(hipStreamSynchronize(d.stream));
+  return TI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t ti_abi_version(void) { return TI_ABI_VERSION; }
+
+const char* ti_last_error(void) { return g_last_error.c_str(); }
+
+int ti_device_count(int32_t* count) {
+  if (!count) return fail(TI_ERR_INVALID, "null count");
+  int n = 0;
+  TI_HIP(hipGetDeviceCount(&n));
+  *count = n;
+  return TI_OK;
+}
+
+int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t n_devices,
+                     ti_forest** out) {
+  if (!out) return fail(TI_ERR_INVALID, "null output handle");
+  *out = nullptr;
+  if (!devices || n_devices <= 0) return fail(TI_ERR_INVALID, "need at least one device");
+  std::vector<int> depth;
+  int rc = validate(desc, &depth);
+  if (rc) return rc;
+  int n_visible = 0;
+  TI_HIP(hipGetDeviceCount(&n_visible));
+  for (int i = 0; i < n_devices; ++i)
+    if (devices[i] < 0 || devices[i] >= n_visible)
+      return fail(TI_ERR_INVALID, "device ordinal " + std::to_string(devices[i]) + " not visible");
+
+  std::unique_ptr<ti_forest> f(new ti_forest());
+  f->T = desc->n_trees;
+  f->F = desc->n_features;
+  f->K = desc->n_groups;
+  f->LW = desc->leaf_width;
+  f->accum = desc->accum_dtype;
+  f->base_first = desc->base_first ? 1 : 0;
+  f->lgb_zero_map = desc->lgb_zero_map ? 1 : 0;
+  f->transform = desc->transform;
+  f->tparam = desc->transform_param;
+  f->divisor = desc->average_divisor;
+  for (int k = 0; k < f->K; ++k) f->base[k] = desc->base_margin[k];
+  for (int64_t i = 0; i < desc->n_nodes; ++i)
+    if (desc->feature[i] >= 0 && (desc->flags[i] & TI_NODE_ZERO_FLIP)) f->zero_rule = 1;
+  f->h_group.assign(f->T, 0);
+  if (f->LW == 1)
+    for (int t = 0; t < f->T; ++t) f->h_group[t] = desc->tree_group[t];
+  f->depth = *std::max_element(depth.begin(), depth.end());
+
+  const size_t acc_sz = f->accum == TI_F64 ? 8 : 4;
+  const int D = f->depth;
+  if (D <= kMaxHeapDepth) {
+    const int NI = (1 << D) - 1, NL = 1 << D;
+    f->layout = 0;
+    f->stride32 = static_cast<int64_t>(align16(sizeof(HeapNode<float>) * NI + acc_sz * NL * f->LW));
+    f->stride64 = static_cast<int64_t>(align16(sizeof(HeapNode<double>) * NI + acc_sz * NL * f->LW));
+    if (f->accum == TI_F64) {
+      pack_heap<float, double>(desc, D, f->stride32, &f->h_heap32, &f->h_heap_leaf_ids);
+      pack_heap<double, double>(desc, D, f->stride64, &f->h_heap64, nullptr);
+    } else {
+      pack_heap<float, float>(desc, D, f->stride32, &f->h_heap32, &f->h_heap_leaf_ids);
+      pack_heap<double, float>(desc, D, f->stride64, &f->h_heap64, nullptr);
+    }
+  } else {
+    f->layout = 1;
+    if (f->accum == TI_F64)
+      pack_explicit<double>(desc, f.get());
+    else
+      pack_explicit<float>(desc, f.get());
+  }
+  for (int i = 0; i < n_devices; ++i) {
+    f->devs.emplace_back(new DeviceForest());
+    rc = upload_device(f.get(), *f->devs.back(), devices[i]);
+    if (rc) {
+      for (auto& d : f->devs) free_device(*d);
+      return rc;
+    }
+  }
+  // host images are no longer needed once every replica is resident
+  f->h_heap32.clear(); f->h_heap32.shrink_to_fit();
+  f->h_heap64.clear(); f->h_heap64.shrink_to_fit();
+  f->h_heap_leaf_ids.clear(); f->h_heap_leaf_ids.shrink_to_fit();
+  f->h_nodes.clear(); f->h_nodes.shrink_to_fit();
+  f->h_thr64.clear(); f->h_thr64.shrink_to_fit();
+  f->h_leaves.clear(); f->h_leaves.shrink_to_fit();
+  *out = f.release();
+  return TI_OK;
+}
+
+int ti_forest_destroy(ti_forest* forest) {
+  if (!forest) return TI_OK;
+  for (auto& d : forest->devs) free_device(*d);
+  delete forest;
+  return TI_OK;
+}
+
+int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
+  if (!f || !info) return fail(TI_ERR_INVALID, "null argument");
+  info->layout = f->layout;
+  info->depth = f->depth;
+  info->n_trees = f->T;
+  info->n_groups = f->K;
+  info->n_features = f->F;
+  info->n_devices = static_cast<int32_t>(f->devs.size());
+  info->device_bytes = f->devs.empty() ? 0 : f->devs[0]->bytes;
+  info->tree_stride_bytes = f->layout == 0 ? f->stride32 : 0;
+  return TI_OK;
+}
+
+int ti_output_shape(const ti_forest* f, int32_t kind, int64_t n_rows, int64_t* out_len,
+                    int32_t* out_dtype) {
+  if (!f || !out_len || !out_dtype) return fail(TI_ERR_INVALID, "null argument");
+  if (kind < TI_OUTPUT_MARGIN || kind > TI_OUTPUT_LEAF) return fail(TI_ERR_INVALID, "bad output kind");
+  if (n_rows < 0) return fail(TI_ERR_INVALID, "negative n_rows");
+  *out_len = n_rows * output_width(f, kind);
+  *out_dtype = output_dtype(f, kind);
+  return TI_OK;
+}
+
+static int check_call(const ti_forest* f, const void* X, int32_t xdt, int64_t rows, int32_t cols,
+                      int64_t stride, int32_t kind, const void* out, int64_t out_len) {
+  if (!f) return fail(TI_ERR_INVALID, "null forest");
+  if (xdt != TI_F32 && xdt != TI_F64) return fail(TI_ERR_INVALID, "x_dtype must be TI_F32 or TI_F64");
+  if (kind < TI_OUTPUT_MARGIN || kind > TI_OUTPUT_LEAF) return fail(TI_ERR_INVALID, "bad output kind");
+  if (rows < 0) return fail(TI_ERR_INVALID, "negative n_rows");
+  if (rows == 0) return TI_OK;
+  if (!X || !out) return fail(TI_ERR_INVALID, "null data pointer");
+  if (cols <= 0) return fail(TI_ERR_INVALID, "n_cols must be > 0");
+  if (stride < cols) return fail(TI_ERR_INVALID, "row_stride < n_cols");
+  if (out_len < rows * output_width(f, kind))
+    return fail(TI_ERR_INVALID, "output buffer too small: need " +
+                                    std::to_string(rows * output_width(f, kind)) + " elements");
+  return TI_OK;
+}
+
+int ti_predict(ti_forest* f, const void* X, int32_t xdt, int64_t rows, int32_t cols,
+               int64_t stride, int32_t kind, void* out, int64_t out_len) {
+  int rc = check_call(f, X, xdt, rows, cols, stride, kind, out, out_len);
+  if (rc || rows == 0) return rc;
+  const int nd = static_cast<int>(f->devs.size());
+  const size_t xs = dtype_size(xdt);
+  const size_t os = dtype_size(output_dtype(f, kind)) * output_width(f, kind);
+  const int64_t per = (rows + nd - 1) / nd;
+  const unsigned char* xb = static_cast<const unsigned char*>(X);
+  unsigned char* ob = static_cast<unsigned char*>(out);
+  if (nd == 1) return predict_shard(f, *f->devs[0], xb, xdt, rows, cols, stride, kind, ob);
+  std::vector<int> rcs(nd, TI_OK);
+  std::vector<std::string> errs(nd);
+  std::vector<std::thread> th;
+  for (int i = 0; i < nd; ++i) {
+    const int64_t r0 = per * i;
+    const int64_t r1 = std::min(rows, r0 + per);
+    if (r0 >= r1) break;
+    th.emplace_back([&, i, r0, r1]() {
+      rcs[i] = predict_shard(f, *f->devs[i], xb + r0 * stride * xs, xdt, r1 - r0, cols, stride,
+                             kind, ob + r0 * os);
+      if (rcs[i]) errs[i] = g_last_error;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int i = 0; i < nd; ++i)
+    if (rcs[i]) return fail(rcs[i], "device slot " + std::to_string(i) + ": " + errs[i]);
+  return TI_OK;
+}
+
+int ti_predict_device(ti_forest* f, int32_t slot, const void* X, int32_t xdt, int64_t rows,
+                      int32_t cols, int64_t stride, int32_t kind, void* out, int64_t out_len,
+                      void* stream) {
+  int rc = check_call(f, X, xdt, rows, cols, stride, kind, out, out_len);
+  if (rc || rows == 0) return rc;
+  if (slot < 0 || slot >= static_cast<int>(f->devs.size()))
+    return fail(TI_ERR_INVALID, "device_slot out of range");
+  DeviceForest& d = *f->devs[slot];
+  TI_HIP(hipSetDevice(d.device));
+  return launch(f, d, X, xdt, rows, cols, stride, kind, out, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,260 @@
+"""LightGBM text model (v2/v3) -> canonical :class:`~kfserving_amd.forest.Forest`.
+
+Replaces ``lgb.Booster(params={"nthread": n}, model_file=.../model.bst)`` at
+python/lgbserver/lgbserver/model.py:39-40 without importing lightgbm (the
+reference pins lightgbm 2.3.1, python/lgbserver/setup.py:37).  Format as in
+the fixture python/lgbserver/lgbserver/example_model/model/model.bst:1-12
+(header), :12-28 (one ``Tree=`` block), :5412 (``end of trees``).
+
+Predict semantics encoded (upstream lightgbm 2.3.1 ``Tree::NumericalDecision``
+and ``GBDT::PredictRaw``): features read as float64; missing type None maps
+NaN to 0.0, Zero sends |x| <= 1e-35 to the default child, NaN sends NaN to the
+default child; otherwise left iff ``x <= threshold``; scores accumulated in
+float64 in tree order, tree t feeding class t mod num_tree_per_iteration.
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import numpy as np
+
+from ..forest import (Forest, MISSING_NAN, MISSING_NONE, MISSING_ZERO, NODE_NAN_LEFT,
+                      NODE_ZERO_FLIP, TI_F64, T_EXP, T_IDENTITY, T_LOG1PEXP, T_SIGMOID,
+                      T_SIGNSQUARE, T_SOFTMAX, concat_trees)
+
+
+class LightGBMFormatError(ValueError):
+    pass
+
+
+def _ints(s: str) -> np.ndarray:
+    return np.array([int(v) for v in s.split()], dtype=np.int64) if s.strip() else \
+        np.zeros(0, dtype=np.int64)
+
+
+def _floats(s: str) -> np.ndarray:
+    return np.array([float(v) for v in s.split()], dtype=np.float64) if s.strip() else \
+        np.zeros(0, dtype=np.float64)
+
+
+def objective_transform(objective: str):
+    """(transform, param) of ObjectiveFunction::ConvertOutput for a model line."""
+    parts = objective.split()
+    name = parts[0] if parts else ""
+    kv = {}
+    flags = set()
+    for p in parts[1:]:
+        if ":" in p:
+            k, v = p.split(":", 1)
+            kv[k] = v
+        else:
+            flags.add(p)
+    if name == "binary":
+        return T_SIGMOID, float(kv.get("sigmoid", 1.0))
+    if name in ("multiclass", "softmax"):
+        return T_SOFTMAX, 1.0
+    if name in ("multiclassova", "multiclass_ova", "ova", "ovr"):
+        return T_SIGMOID, float(kv.get("sigmoid", 1.0))
+    if name in ("cross_entropy", "xentropy"):
+        return T_SIGMOID, 1.0
+    if name in ("cross_entropy_lambda", "xentlambda"):
+        return T_LOG1PEXP, 1.0
+    if name in ("poisson", "gamma", "tweedie"):
+        return T_EXP, 1.0
+    if name in ("regression", "regression_l2", "l2", "mean_squared_error", "mse") and \
+            "sqrt" in flags:
+        return T_SIGNSQUARE, 1.0
+    return T_IDENTITY, 1.0
+
+
+def _node_flags(decision_type: np.ndarray, threshold: np.ndarray) -> np.ndarray:
+    if np.any(decision_type & 1):
+        raise LightGBMFormatError("categorical splits are not supported yet")
+    default_left = (decision_type & 2) != 0
+    missing = (decision_type >> 2) & 3
+    zero_left = 0.0 <= threshold             # where a NaN->0 / zero input lands
+    nan_left = np.where(missing == MISSING_NONE, zero_left, default_left)
+    zero_flip = (missing == MISSING_ZERO) & (default_left != zero_left)
+    flags = np.where(nan_left, NODE_NAN_LEFT, 0) | np.where(zero_flip, NODE_ZERO_FLIP, 0)
+    if np.any((missing != MISSING_NONE) & (missing != MISSING_ZERO) & (missing != MISSING_NAN)):
+        raise LightGBMFormatError("unknown missing type")
+    return flags.astype(np.uint8)
+
+
+def _tree(block: Dict[str, str]) -> dict:
+    num_leaves = int(block["num_leaves"])
+    leaf_value = _floats(block["leaf_value"])
+    if leaf_value.shape[0] != num_leaves:
+        raise LightGBMFormatError("leaf_value length != num_leaves")
+    if int(block.get("num_cat", "0")) > 0:
+        raise LightGBMFormatError("categorical splits are not supported yet")
+    if block.get("is_linear", "0").strip() not in ("", "0"):
+        raise LightGBMFormatError("linear trees are not supported")
+    if num_leaves == 1:
+        return {"feature": np.array([-1]), "threshold": np.zeros(1), "flags": np.zeros(1),
+                "left": np.array([-1]), "right": np.array([-1]), "leaf_id": np.array([0]),
+                "leaf_value": leaf_value.reshape(1, 1)}
+    n_int = num_leaves - 1
+    feat = _ints(block["split_feature"])
+    thr = _floats(block["threshold"])
+    dt = _ints(block["decision_type"])
+    lc = _ints(block["left_child"])
+    rc = _ints(block["right_child"])
+    for name, arr in (("split_feature", feat), ("threshold", thr), ("decision_type", dt),
+                      ("left_child", lc), ("right_child", rc)):
+        if arr.shape[0] != n_int:
+            raise LightGBMFormatError(f"{name} length != num_leaves - 1")
+    n = n_int + num_leaves
+    # canonical numbering: internal nodes 0..n_int-1, leaf j at n_int + j
+    left = np.where(lc >= 0, lc, n_int + ~lc)
+    right = np.where(rc >= 0, rc, n_int + ~rc)
+    return {
+        "feature": np.concatenate([feat, np.full(num_leaves, -1)]),
+        "threshold": np.concatenate([thr, np.zeros(num_leaves)]),
+        "flags": np.concatenate([_node_flags(dt, thr), np.zeros(num_leaves, dtype=np.uint8)]),
+        "left": np.concatenate([left, np.full(num_leaves, -1)]),
+        "right": np.concatenate([right, np.full(num_leaves, -1)]),
+        "leaf_id": np.concatenate([np.full(n_int, -1), np.arange(num_leaves)]),
+        "leaf_value": np.concatenate([np.zeros(n_int), leaf_value]).reshape(n, 1),
+    }
+
+
+def parse_lightgbm_text(text: str) -> Forest:
+    lines = text.splitlines()
+    header: Dict[str, str] = {}
+    flags_present = set()
+    i = 0
+    while i < len(lines) and not lines[i].startswith("Tree="):
+        line = lines[i].strip()
+        if "=" in line:
+            k, v = line.split("=", 1)
+            header[k.strip()] = v.strip()
+        elif line:
+            flags_present.add(line)
+        i += 1
+    if "version" not in header and "tree" not in flags_present:
+        raise LightGBMFormatError("not a LightGBM text model")
+    blocks: List[Dict[str, str]] = []
+    cur = None
+    for line in lines[i:]:
+        s = line.strip()
+        if s.startswith("Tree="):
+            cur = {}
+            blocks.append(cur)
+        elif s == "end of trees":
+            break
+        elif cur is not None and "=" in s:
+            k, v = s.split("=", 1)
+            cur[k] = v
+    if not blocks:
+        raise LightGBMFormatError("model has no trees")
+    trees = [_tree(b) for b in blocks]
+    cat = concat_trees(trees, 1)
+    ntpi = int(header.get("num_tree_per_iteration", header.get("num_class", "1")))
+    K = max(1, ntpi)
+    n_features = int(header.get("max_feature_idx", "-1")) + 1
+    used = cat["feature"][cat["feature"] >= 0]
+    if used.size:
+        n_features = max(n_features, int(used.max()) + 1)
+    objective = header.get("objective", "")
+    transform, tparam = objective_transform(objective)
+    average = "average_output" in flags_present or header.get("average_output") is not None
+    n_iter = len(trees) // K
+    names = header.get("feature_names", "").split() or None
+    return Forest(
+        n_features=max(n_features, 1), n_groups=K, leaf_width=1, accum_dtype=TI_F64,
+        base_first=True, lgb_zero_map=True,
+        tree_offset=cat["tree_offset"],
+        tree_group=(np.arange(len(trees)) % K).astype(np.int32),
+        feature=cat["feature"], threshold=cat["threshold"], flags=cat["flags"],
+        left=cat["left"], right=cat["right"], leaf_id=cat["leaf_id"],
+        leaf_value=cat["leaf_value"], base_margin=np.zeros(K),
+        average_divisor=float(n_iter) if average and n_iter > 0 else 1.0,
+        transform=transform, transform_param=tparam, input_dtype=TI_F64,
+        library="lightgbm", objective=objective, feature_names=names,
+        meta={"version": header.get("version", ""), "num_class": int(header.get("num_class", 1))},
+    ).contiguous()
+
+
+def load_lightgbm_model(path: str) -> Forest:
+    with open(path, "r") as fh:
+        return parse_lightgbm_text(fh.read())
+
+
+# ------------------------------------------------------------------ writer
+def _fmt(v: float) -> str:
+    return repr(float(v))
+
+
+def write_lightgbm_text(path: str, trees: List[dict], n_features: int, objective: str,
+                        num_class: int = 1, feature_names=None) -> None:
+    """Write a LightGBM v3 text model (subset the loader reads).
+
+    ``trees`` hold LightGBM Tree arrays: ``split_feature, threshold,
+    decision_type, left_child, right_child`` (negative = ~leaf) and
+    ``leaf_value``.  Used for the synthetic leaf-wise benchmark models.
+    """
+    names = feature_names or [f"Column_{j}" for j in range(n_features)]
+    out = ["tree", "version=v3", f"num_class={num_class}",
+           f"num_tree_per_iteration={num_class if num_class > 1 else 1}",
+           "label_index=0", f"max_feature_idx={n_features - 1}", f"objective={objective}",
+           "feature_names=" + " ".join(names), "feature_infos=" + " ".join(["none"] * n_features),
+           "tree_sizes=" + " ".join(["0"] * len(trees)), ""]
+    for i, t in enumerate(trees):
+        nl = len(t["leaf_value"])
+        out.append(f"Tree={i}")
+        out.append(f"num_leaves={nl}")
+        out.append("num_cat=0")
+        if nl > 1:
+            out.append("split_feature=" + " ".join(str(int(v)) for v in t["split_feature"]))
+            out.append("split_gain=" + " ".join("1" for _ in t["split_feature"]))
+            out.append("threshold=" + " ".join(_fmt(v) for v in t["threshold"]))
+            out.append("decision_type=" + " ".join(str(int(v)) for v in t["decision_type"]))
+            out.append("left_child=" + " ".join(str(int(v)) for v in t["left_child"]))
+            out.append("right_child=" + " ".join(str(int(v)) for v in t["right_child"]))
+        out.append("leaf_value=" + " ".join(_fmt(v) for v in t["leaf_value"]))
+        out.append("shrinkage=1")
+        out.append("")
+        out.append("")
+    out.append("end of trees")
+    out.append("")
+    with open(path, "w") as fh:
+        fh.write("\n".join(out))
+
+
+def synthetic_leafwise_trees(n_trees: int, num_leaves: int, n_features: int, seed: int,
+                             missing_types=(MISSING_NONE, MISSING_ZERO, MISSING_NAN)) -> List[dict]:
+    """Seeded leaf-wise trees: grow by splitting a
+    random current leaf until ``num_leaves``; thresholds ~ N(0,1) as float64,
+    decision_type draws default_left and a missing type."""
+    rng = np.random.default_rng(seed)
+    trees = []
+    mts = np.asarray(missing_types)
+    for _ in range(n_trees):
+        n_int = num_leaves - 1
+        feat = rng.integers(0, n_features, size=n_int)
+        thr = rng.standard_normal(n_int)
+        dl = rng.integers(0, 2, size=n_int)
+        mt = mts[rng.integers(0, len(mts), size=n_int)]
+        dtype_ = (dl << 1) | (mt << 2)
+        left = np.zeros(n_int, dtype=np.int64)
+        right = np.zeros(n_int, dtype=np.int64)
+        # leaves as (parent, side); start: root split with two leaves 0, 1
+        leaf_owner = [(0, 0), (0, 1)]
+        left[0], right[0] = ~0, ~1
+        for node in range(1, n_int):
+            j = int(rng.integers(0, len(leaf_owner)))   # split leaf j
+            parent, side = leaf_owner[j]
+            if side == 0:
+                left[parent] = node
+            else:
+                right[parent] = node
+            new_leaf = len(leaf_owner)
+            leaf_owner[j] = (node, 0)
+            leaf_owner.append((node, 1))
+            left[node] = ~j
+            right[node] = ~new_leaf
+        trees.append({"split_feature": feat, "threshold": thr, "decision_type": dtype_,
+                      "left_child": left, "right_child": right,
+                      "leaf_value": rng.uniform(-0.05, 0.05, size=num_leaves)})
+    return trees

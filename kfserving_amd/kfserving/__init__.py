@@ -1,0 +1,5 @@
+"""Mirror of the python/kfserving model-server API the tree plugins plug into."""
+from .errors import HTTPError  # noqa: F401
+from .kfmodel import KFModel  # noqa: F401
+from .kfmodel_repository import KFModelRepository, MODEL_MOUNT_DIRS  # noqa: F401
+from .storage import Storage  # noqa: F401

@@ -1,0 +1,46 @@
+"""LightGBMModel -- GPU drop-in for python/lgbserver/lgbserver/model.py:25-54.
+
+Same constructor (name, model_dir, nthread, booster=None) and ``inputs``
+request format: one DataFrame per element with ``columns=feature_name()``,
+rows concatenated (:46-50), then one libtreeinfer call in float64 where the
+reference called ``Booster.predict`` (:51).
+"""
+import os
+from typing import Dict
+
+from ..formats.lightgbm_format import load_lightgbm_model
+from ..forest import Forest
+from ..kfserving.kfmodel import KFModel
+from ..kfserving.storage import Storage
+from ..tree_model import GPUForestMixin, lgb_matrix_from_inputs
+
+BOOSTER_FILE = "model.bst"
+
+
+class LightGBMModel(GPUForestMixin, KFModel):
+    def __init__(self, name: str, model_dir: str, nthread: int, booster: Forest = None):
+        super().__init__(name)
+        self.name = name
+        self.model_dir = model_dir
+        self.nthread = nthread
+        if booster is not None:
+            self._set_forest(booster)
+            self.ready = True
+
+    def load(self) -> bool:
+        model_file = os.path.join(Storage.download(self.model_dir), BOOSTER_FILE)
+        self._set_forest(load_lightgbm_model(model_file))
+        self.ready = True
+        return self.ready
+
+    def feature_name(self):
+        names = self._forest.feature_names
+        return list(names) if names else [f"Column_{j}" for j in range(self._forest.n_features)]
+
+    def predict(self, request: Dict) -> Dict:
+        try:
+            X = lgb_matrix_from_inputs(request["inputs"], self.feature_name())
+            result = self.predict_matrix(X)
+            return {"predictions": result.tolist()}
+        except Exception as e:
+            raise Exception("Failed to predict %s" % e)

@@ -1,0 +1,72 @@
+"""SKLearnModel -- GPU drop-in for python/sklearnserver/sklearnserver/model.py:25-54.
+
+Same constructor (name, model_dir) and ``instances`` request format.  ``load``
+finds model.joblib / .pkl / .pickle like the reference (:21-41; these files
+are the user's own model, loaded with joblib exactly as the reference does)
+or the pickle-free ``model.npz`` tree-array export, and flattens a
+RandomForest / ExtraTrees / DecisionTree estimator; ``predict`` runs the
+trees through libtreeinfer where the reference called ``_model.predict``.
+"""
+import os
+from typing import Dict
+
+import numpy as np
+
+from ..formats.sklearn_format import forest_from_sklearn, load_tree_arrays
+from ..kfserving.kfmodel import KFModel
+from ..kfserving.storage import Storage
+from ..tree_model import GPUForestMixin
+
+MODEL_BASENAME = "model"
+MODEL_EXTENSIONS = [".joblib", ".pkl", ".pickle"]
+ARRAYS_EXTENSION = ".npz"
+
+
+class SKLearnModel(GPUForestMixin, KFModel):  # pylint:disable=c-extension-no-member
+    def __init__(self, name: str, model_dir: str):
+        super().__init__(name)
+        self.name = name
+        self.model_dir = model_dir
+        self.ready = False
+
+    def load(self) -> bool:
+        model_path = Storage.download(self.model_dir)
+        paths = [os.path.join(model_path, MODEL_BASENAME + ext) for ext in MODEL_EXTENSIONS]
+        for path in paths:
+            if os.path.exists(path):
+                import joblib
+                self._set_forest(forest_from_sklearn(joblib.load(path)))
+                self.ready = True
+                break
+        if not self.ready:
+            npz = os.path.join(model_path, MODEL_BASENAME + ARRAYS_EXTENSION)
+            if os.path.exists(npz):
+                self._set_forest(load_tree_arrays(npz))
+                self.ready = True
+        return self.ready
+
+    def predict(self, request: Dict) -> Dict:
+        instances = request["instances"]
+        try:
+            inputs = np.array(instances)
+        except Exception as e:
+            raise Exception(
+                "Failed to initialize NumPy array from inputs: %s, %s" % (e, instances))
+        try:
+            f = self._forest
+            X = np.asarray(inputs, dtype=np.float64)
+            if X.ndim != 2:
+                raise ValueError("Expected 2D array, got %dD array instead" % X.ndim)
+            if X.shape[1] != f.n_features:
+                raise ValueError("X has %d features, but %s is expecting %d features as input."
+                                 % (X.shape[1], f.objective, f.n_features))
+            if np.isinf(X).any():
+                raise ValueError("Input X contains infinity or a value too large for "
+                                 "dtype('float32').")
+            result = self.predict_matrix(X)
+            classes = f.meta.get("classes")
+            if classes is not None:
+                result = np.asarray(classes).take(result.astype(np.int64), axis=0)
+            return {"predictions": result.tolist()}
+        except Exception as e:
+            raise Exception("Failed to predict %s" % e)

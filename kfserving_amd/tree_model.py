@@ -1,0 +1,95 @@
+"""Shared GPU plumbing of the three tree plugins.
+
+The reference loads the model *before* ``KFServer.start`` forks its workers
+(python/xgbserver/xgbserver/__main__.py:37-46, kfserver.py:99), so the parsed
+forest must stay a plain host object until the first predict in each worker
+process: :class:`GPUForestMixin` creates the device replica lazily
+(post-fork), once, under a lock.  Input conversion helpers reproduce how each
+library turns a JSON request into a feature matrix.
+"""
+from __future__ import annotations
+
+import threading
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .engine import DeviceForest
+from .forest import OUT_PREDICT, Forest
+
+
+class GPUForestMixin:
+    _forest: Optional[Forest] = None
+    _device_forest: Optional[DeviceForest] = None
+    devices: Optional[Sequence[int]] = None
+
+    def _set_forest(self, forest: Forest) -> None:
+        self._forest = forest
+        self._device_forest = None
+        if not hasattr(self, "_dev_lock"):
+            self._dev_lock = threading.Lock()
+
+    def device_forest(self) -> DeviceForest:
+        dfo = self._device_forest
+        if dfo is None:
+            if not hasattr(self, "_dev_lock"):
+                self._dev_lock = threading.Lock()
+            with self._dev_lock:
+                if self._device_forest is None:
+                    if self._forest is None:
+                        raise RuntimeError("model is not loaded")
+                    self._device_forest = DeviceForest(self._forest, self.devices)
+                dfo = self._device_forest
+        return dfo
+
+    def predict_matrix(self, X: np.ndarray, kind: int = OUT_PREDICT) -> np.ndarray:
+        return self.device_forest().predict(X, kind)
+
+
+def xgb_matrix_from_list(instances) -> np.ndarray:
+    """``xgb.DMatrix(list)`` as xgboost 0.82 builds it (xgbserver/model.py:46).
+
+    A python list goes through ``scipy.sparse.csr_matrix(data)``: zeros are not
+    stored (missing -> default child) while NaN is stored as a value, which never
+    satisfies ``x < split`` (always the right child).  Encoded for the canonical
+    kernel as 0 -> NaN (missing) and NaN -> +inf (right at every split).
+    """
+    X = np.asarray(instances, dtype=np.float64)
+    if X.ndim == 1:
+        X = X.reshape(1, -1)
+    if X.ndim != 2:
+        raise ValueError(f"expected a list of rows, got shape {X.shape}")
+    absent = X == 0
+    present_nan = np.isnan(X)
+    X32 = X.astype(np.float32)
+    X32[absent] = np.nan
+    X32[present_nan] = np.inf
+    return X32
+
+
+def lgb_matrix_from_inputs(inputs: List[dict], feature_names: List[str]) -> np.ndarray:
+    """``pd.concat([pd.DataFrame(i, columns=booster.feature_name()) ...])`` then
+    lightgbm's float conversion (lgbserver/model.py:46-51): columns chosen by
+    name, absent columns NaN, extra keys dropped, float64."""
+    fast = []
+    for inp in inputs:
+        if not isinstance(inp, dict) or not all(isinstance(v, (list, tuple))
+                                                for v in inp.values()):
+            fast = None
+            break
+        n = {len(inp[k]) for k in feature_names if k in inp}
+        if len(n) > 1:
+            fast = None
+            break
+        rows = n.pop() if n else 0
+        cols = [np.asarray(inp[k], dtype=np.float64) if k in inp else np.full(rows, np.nan)
+                for k in feature_names]
+        fast.append(np.stack(cols, axis=1) if cols else np.zeros((rows, 0)))
+    if fast is not None:
+        return np.concatenate(fast, axis=0) if fast else np.zeros((0, len(feature_names)))
+    import pandas as pd
+    df = pd.concat([pd.DataFrame(i, columns=feature_names) for i in inputs], axis=0)
+    for dt in df.dtypes:
+        if not (np.issubdtype(dt, np.number) or dt == bool):
+            raise ValueError("DataFrame.dtypes for data must be int, float or bool")
+    return df.to_numpy(dtype=np.float64)

@@ -1,0 +1,48 @@
+"""XGBoostModel -- GPU drop-in for python/xgbserver/xgbserver/model.py:24-50.
+
+Same constructor (name, model_dir, nthread, booster=None), same ``load`` /
+``predict`` contract and response shape; ``Booster.predict`` on a DMatrix
+(:46-47) becomes one libtreeinfer call.  ``nthread`` is accepted for CLI and
+repository compatibility; the device, not host threads, runs the trees.
+"""
+import os
+from typing import Dict
+
+import numpy as np
+
+from ..formats.xgboost_format import load_xgboost_model
+from ..forest import Forest
+from ..kfserving.kfmodel import KFModel
+from ..kfserving.storage import Storage
+from ..tree_model import GPUForestMixin, xgb_matrix_from_list
+
+BOOSTER_FILE = "model.bst"
+
+
+class XGBoostModel(GPUForestMixin, KFModel):
+    def __init__(self, name: str, model_dir: str, nthread: int, booster: Forest = None):
+        super().__init__(name)
+        self.name = name
+        self.model_dir = model_dir
+        self.nthread = nthread
+        if booster is not None:
+            self._set_forest(booster)
+            self.ready = True
+
+    def load(self) -> bool:
+        model_file = os.path.join(Storage.download(self.model_dir), BOOSTER_FILE)
+        self._set_forest(load_xgboost_model(model_file))
+        self.ready = True
+        return self.ready
+
+    def predict(self, request: Dict) -> Dict:
+        try:
+            instances = request["instances"]
+            if isinstance(instances, np.ndarray):
+                X = instances                      # DMatrix(ndarray): NaN = missing
+            else:
+                X = xgb_matrix_from_list(instances)   # DMatrix(list) semantics
+            result = self.predict_matrix(X)
+            return {"predictions": result.tolist()}
+        except Exception as e:
+            raise Exception("Failed to predict %s" % e)

@@ -1,0 +1,77 @@
+"""Numpy evaluator of the canonical forest semantics (include/treeinfer.h) --
+test helper only.  It lets CPU tests check that each loader's canonical
+encoding (thresholds, NaN / zero flags, leaf payloads, base, transform)
+reproduces the oracle, independently of the GPU kernels."""
+import numpy as np
+
+from kfserving_amd.forest import (NODE_NAN_LEFT, NODE_ZERO_FLIP, OUT_LEAF, OUT_MARGIN,
+                                  T_ARGMAX, T_EXP, T_HINGE, T_IDENTITY, T_SIGMOID, T_SOFTMAX,
+                                  TI_F32, round_down_f32)
+
+
+def leaves(f, X):
+    X = np.asarray(X)
+    f32 = X.dtype == np.float32
+    if f.lgb_zero_map:
+        X = np.where(np.abs(X.astype(np.float64)) <= float(np.float32(1e-35)), 0, X).astype(X.dtype)
+    thr = round_down_f32(f.threshold) if f32 else f.threshold
+    rows = X.shape[0]
+    out = np.zeros((rows, f.n_trees), dtype=np.int64)
+    for t in range(f.n_trees):
+        b = int(f.tree_offset[t])
+        node = np.zeros(rows, dtype=np.int64)
+        while True:
+            act = f.feature[b + node] >= 0
+            if not act.any():
+                break
+            idx = np.nonzero(act)[0]
+            g = b + node[idx]
+            fi = f.feature[g]
+            x = np.where(fi < X.shape[1], X[idx, np.minimum(fi, X.shape[1] - 1)], np.nan)
+            left = x <= thr[g]
+            left = np.where(np.isnan(x), (f.flags[g] & NODE_NAN_LEFT) != 0, left)
+            flip = (x == 0) & ((f.flags[g] & NODE_ZERO_FLIP) != 0)
+            left = np.where(flip, ~left, left)
+            node[idx] = np.where(left, f.left[g], f.right[g])
+        out[:, t] = node
+    return out
+
+
+def predict(f, X, kind=1):
+    lv = leaves(f, X)
+    if kind == OUT_LEAF:
+        return f.leaf_id[f.tree_offset[:-1][None, :] + lv]
+    acc_t = np.float32 if f.accum_dtype == TI_F32 else np.float64
+    K = f.n_groups
+    rows = lv.shape[0]
+    acc = np.zeros((rows, K), dtype=acc_t)
+    if f.base_first:
+        acc += f.base_margin.astype(acc_t)
+    for t in range(f.n_trees):
+        v = f.leaf_value[f.tree_offset[t] + lv[:, t]].astype(acc_t)
+        if f.leaf_width == 1:
+            g = f.tree_group[t]
+            acc[:, g] = acc[:, g] + v[:, 0]
+        else:
+            acc = acc + v
+    m = acc if f.base_first else (f.base_margin.astype(acc_t) + acc)
+    if f.average_divisor != 1.0:
+        m = m / acc_t(f.average_divisor)
+    if kind == OUT_MARGIN or f.transform == T_IDENTITY:
+        return m if K > 1 else m[:, 0]
+    if f.transform == T_ARGMAX:
+        return np.argmax(m, axis=1).astype(acc_t)
+    if f.transform == T_SOFTMAX:
+        wmax = m.max(axis=1, keepdims=True)
+        e = np.exp(m - wmax).astype(acc_t)
+        return e / e.astype(np.float64).sum(axis=1, keepdims=True).astype(acc_t)
+    if f.transform == T_SIGMOID:
+        p = acc_t(1) / (acc_t(1) + np.exp(-(acc_t(f.transform_param) * m)))
+        return p if K > 1 else p[:, 0]
+    if f.transform == T_HINGE:
+        p = np.where(m > 0, acc_t(1), acc_t(0))
+        return p if K > 1 else p[:, 0]
+    if f.transform == T_EXP:
+        p = np.exp(m)
+        return p if K > 1 else p[:, 0]
+    raise NotImplementedError(f.transform)

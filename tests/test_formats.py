@@ -1,0 +1,142 @@
+"""Loaders -> canonical forest, checked on CPU against the oracle through the
+canonical-semantics evaluator (tests/canon_eval.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from kfserving_amd.forest import OUT_LEAF, OUT_MARGIN, OUT_PREDICT, round_down_f32
+from kfserving_amd.formats import (forest_from_sklearn, load_lightgbm_model, load_tree_arrays,
+                                   load_xgboost_model, parse_xgboost_bytes)
+from kfserving_amd.formats import xgboost_format as xf
+from kfserving_amd.formats import lightgbm_format as lf
+from kfserving_amd.tree_model import lgb_matrix_from_inputs, xgb_matrix_from_list
+from oracle import lgb_ref, xgb_ref
+from tests import canon_eval
+
+
+def _iris():
+    from sklearn.datasets import load_iris
+    return load_iris()["data"]
+
+
+@pytest.mark.parametrize("name", ["xgb_iris_legacy_082.bst", "xgb_iris_binf_1x.bst"])
+def test_xgb_fixture_canonical_matches_oracle(golden, name):
+    path = os.path.join(golden, name)
+    f = load_xgboost_model(path)
+    assert f.meta["trailing_bytes"] == 0
+    m = xgb_ref.read_xgb_binary(path)
+    X = _iris().astype(np.float32)
+    assert f.n_trees == 100 and f.n_groups == 10
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_MARGIN),
+                                  xgb_ref.predict(m, X, output_margin=True))
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_PREDICT), xgb_ref.predict(m, X))
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_LEAF), xgb_ref.leaf_index(m, X))
+
+
+def test_lgb_fixture_canonical_matches_oracle(golden):
+    path = os.path.join(golden, "lgb_iris_v3.txt")
+    f = load_lightgbm_model(path)
+    m = lgb_ref.read_lgb_text(path)
+    X = _iris()
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_MARGIN),
+                                  lgb_ref.predict(m, X, raw_score=True))
+    np.testing.assert_allclose(canon_eval.predict(f, X, OUT_PREDICT), lgb_ref.predict(m, X),
+                               rtol=1e-12)
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_LEAF), lgb_ref.leaf_index(m, X))
+    # float32 input path: exact via round_down_f32 thresholds
+    X32 = X.astype(np.float32)
+    np.testing.assert_array_equal(canon_eval.predict(f, X32, OUT_MARGIN),
+                                  lgb_ref.predict(m, X32.astype(np.float64), raw_score=True))
+
+
+def test_lgb_synthetic_missing_types(golden):
+    g = np.load(os.path.join(golden, "lgb_synth.npz"))
+    trees = lf.synthetic_leafwise_trees(20, 63, 28, seed=3)
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, 28, "binary sigmoid:1")
+        f = load_lightgbm_model(p)
+        m = lgb_ref.read_lgb_text(p)
+    np.testing.assert_array_equal(canon_eval.predict(f, g["X"], OUT_MARGIN), g["raw"])
+    np.testing.assert_array_equal(lgb_ref.predict(m, g["X"], raw_score=True), g["raw"])
+    np.testing.assert_array_equal(canon_eval.predict(f, g["X"], OUT_LEAF), g["leaf"])
+
+
+def test_xgb_writers_roundtrip(tmp_path):
+    trees, ti = xf.synthetic_complete_trees(12, 5, 10, seed=4, num_class=3)
+    pb = str(tmp_path / "m.bst")
+    pj = str(tmp_path / "m.json")
+    xf.write_legacy_binary(pb, trees, ti, 10, 3, 0.5, "multi:softprob")
+    xf.write_json_model(pj, trees, ti, 10, 3, 0.5, "multi:softprob")
+    fb, fj = load_xgboost_model(pb), load_xgboost_model(pj)
+    m = xgb_ref.read_xgb_binary(pb)
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((300, 10)).astype(np.float32)
+    X[rng.random(X.shape) < 0.05] = np.nan
+    want = xgb_ref.predict(m, X, output_margin=True)
+    np.testing.assert_array_equal(canon_eval.predict(fb, X, OUT_MARGIN), want)
+    np.testing.assert_array_equal(canon_eval.predict(fj, X, OUT_MARGIN), want)  # base 0.5 identity
+
+
+def test_xgb_threshold_encoding_edges():
+    s = np.array([0.0, -0.0, 1.0, np.float32(1e-45), np.inf, -np.inf], dtype=np.float32)
+    t = xf.xgb_threshold(s)
+    xs = np.array([0.0, -0.0, 1.0, np.float32(1e-45), 0.99999994, np.inf, -np.inf, 3.0],
+                  dtype=np.float32)
+    for si, ti in zip(s, t):
+        assert np.array_equal(xs < si, xs.astype(np.float64) <= ti), (si, ti)
+
+
+def test_round_down_f32_exact():
+    rng = np.random.default_rng(1)
+    t = np.concatenate([rng.standard_normal(1000), [3.1500000000000004, 1e300, -1e300, 0.0,
+                                                    np.inf, -np.inf, 1e-45, 5e-324]])
+    r = round_down_f32(t)
+    x = np.concatenate([r, np.nextafter(r, np.float32(np.inf)), rng.standard_normal(1000).astype(np.float32)])
+    for ti, ri in zip(t, r):
+        assert np.array_equal(x.astype(np.float64) <= ti, x <= ri)
+
+
+def test_sklearn_arrays_roundtrip(golden):
+    f = load_tree_arrays(os.path.join(golden, "sk_rf_reg_model.npz"))
+    g = np.load(os.path.join(golden, "sk_rf_reg.npz"))
+    np.testing.assert_array_equal(canon_eval.predict(f, g["X"], OUT_PREDICT), g["predict"])
+    np.testing.assert_array_equal(canon_eval.predict(f, g["X"], OUT_LEAF), g["apply"])
+    fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
+    gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
+    np.testing.assert_array_equal(canon_eval.predict(fc, gc["X"], OUT_MARGIN), gc["predict_proba"])
+    lab = fc.meta["classes"].take(canon_eval.predict(fc, gc["X"], OUT_PREDICT).astype(int))
+    np.testing.assert_array_equal(lab, gc["predict"])
+
+
+def test_sklearn_live_estimator():
+    from sklearn.ensemble import ExtraTreesRegressor
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((400, 6)).astype(np.float32)
+    y = X[:, 0] - X[:, 1] ** 2
+    est = ExtraTreesRegressor(n_estimators=5, random_state=0).fit(X, y)
+    f = forest_from_sklearn(est)
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_PREDICT), est.predict(X))
+
+
+def test_xgb_list_semantics():
+    X = xgb_matrix_from_list([[0.0, 1.5, float("nan"), -0.0]])
+    assert np.isnan(X[0, 0]) and X[0, 1] == np.float32(1.5) and np.isinf(X[0, 2])
+    assert np.isnan(X[0, 3])
+    assert xgb_matrix_from_list([1.0, 2.0]).shape == (1, 2)
+
+
+def test_lgb_inputs_by_name():
+    names = ["a", "b", "c"]
+    X = lgb_matrix_from_inputs([{"c": [3.0], "a": [1.0], "x": [9.0]}], names)
+    assert X.shape == (1, 3) and X[0, 0] == 1.0 and np.isnan(X[0, 1]) and X[0, 2] == 3.0
+    X = lgb_matrix_from_inputs([{"a": {"0": 1.0}, "b": {"0": 2}, "c": {"0": 3}}] * 2, names)
+    assert X.tolist() == [[1.0, 2.0, 3.0], [1.0, 2.0, 3.0]]
+
+
+def test_malformed_xgb_rejected():
+    with pytest.raises(ValueError):
+        parse_xgboost_bytes(b"\x00" * 100)

@@ -1,0 +1,273 @@
+"""GPU parity: libtreeinfer (through the C ABI) vs the oracle / sklearn itself.
+
+Bar (BASELINE.json north_star): bit-exact leaf indices and class labels;
+margins and probabilities within 1e-5 relative.  Where the accumulation order
+is the library's own (XGBoost float32 sequential sum, LightGBM / sklearn
+float64 sequential sum) the margins are compared bit-exactly.
+"""
+import json
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from kfserving_amd.engine import DeviceForest, TreeInferError
+from kfserving_amd.forest import OUT_LEAF, OUT_MARGIN, OUT_PREDICT
+from kfserving_amd.formats import (load_lightgbm_model, load_tree_arrays, load_xgboost_model)
+from kfserving_amd.formats import lightgbm_format as lf
+from kfserving_amd.formats import xgboost_format as xf
+from oracle import lgb_ref, port, xgb_ref
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5   # north_star tolerance for transformed outputs
+
+
+def _model_dir(golden, fname, target="model.bst"):
+    d = tempfile.mkdtemp()
+    os.symlink(os.path.join(golden, fname), os.path.join(d, target))
+    return d
+
+
+def _iris_instances(golden):
+    with open(os.path.join(golden, "iris_input.json")) as fh:
+        return json.load(fh)["instances"]
+
+
+# ------------------------------------------------------------ known answers
+def test_xgbserver_known_answers(golden):
+    from kfserving_amd.xgbserver import XGBoostModel
+    model = XGBoostModel("model", _model_dir(golden, "xgb_iris_legacy_082.bst"), 1)
+    model.load()
+    # python/xgbserver/xgbserver/test_model.py:42-44
+    assert model.predict({"instances": [[5.1, 3.5, 1.4, 0.2]]})["predictions"] == [0]
+    # test/e2e/predictor/test_xgboost.py:67-68
+    assert model.predict({"instances": _iris_instances(golden)})["predictions"] == [1, 1]
+    m2 = XGBoostModel("m2", _model_dir(golden, "xgb_iris_binf_1x.bst"), 1)
+    m2.load()
+    assert m2.predict({"instances": _iris_instances(golden)})["predictions"] == [1.0, 1.0]
+
+
+def test_lgbserver_known_answers(golden):
+    from kfserving_amd.lgbserver import LightGBMModel
+    model = LightGBMModel("model", _model_dir(golden, "lgb_iris_v3.txt"), 1)
+    model.load()
+    request = {"x": {0: 1.1}, 'sepal_width_(cm)': {0: 3.5}, 'petal_length_(cm)': {0: 1.4},
+               'petal_width_(cm)': {0: 0.2}, 'sepal_length_(cm)': {0: 5.1}}
+    response = model.predict({"inputs": [request, request]})
+    assert np.argmax(response["predictions"][0]) == 0       # lgbserver/test_model.py:43-47
+    with open(os.path.join(golden, "iris_input_v3.json")) as fh:
+        res = model.predict(json.load(fh))
+    assert res["predictions"][0][0] > 0.5                    # test_lightgbm.py:65-67
+    m = lgb_ref.read_lgb_text(os.path.join(golden, "lgb_iris_v3.txt"))
+    want = lgb_ref.predict(m, lgb_ref.rows_from_inputs(m, [request]))
+    np.testing.assert_allclose(response["predictions"][0], want[0], rtol=RTOL)
+
+
+# ---------------------------------------------------------------- fixtures
+@pytest.mark.parametrize("name", ["xgb_iris_legacy_082.bst", "xgb_iris_binf_1x.bst"])
+def test_xgb_fixture_full_iris(golden, name):
+    from sklearn.datasets import load_iris
+    path = os.path.join(golden, name)
+    f = load_xgboost_model(path)
+    m = xgb_ref.read_xgb_binary(path)
+    X = load_iris()["data"].astype(np.float32)
+    dev = DeviceForest(f, [0])
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), xgb_ref.predict(m, X, output_margin=True))
+    assert np.array_equal(dev.predict(X, OUT_PREDICT), xgb_ref.predict(m, X))
+    assert np.array_equal(dev.predict(X, OUT_LEAF), xgb_ref.leaf_index(m, X))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lgb_fixture_full_iris(golden, dtype):
+    from sklearn.datasets import load_iris
+    path = os.path.join(golden, "lgb_iris_v3.txt")
+    f = load_lightgbm_model(path)
+    m = lgb_ref.read_lgb_text(path)
+    X = load_iris()["data"].astype(dtype)
+    dev = DeviceForest(f, [0])
+    Xd = X.astype(np.float64)
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), lgb_ref.predict(m, Xd, raw_score=True))
+    np.testing.assert_allclose(dev.predict(X, OUT_PREDICT), lgb_ref.predict(m, Xd), rtol=RTOL)
+    assert np.array_equal(dev.predict(X, OUT_LEAF), lgb_ref.leaf_index(m, Xd))
+
+
+# -------------------------------------------------------- synthetic goldens
+def test_xgb_synthetic_golden(golden):
+    g = np.load(os.path.join(golden, "xgb_synth.npz"))
+    trees, ti = xf.synthetic_complete_trees(40, 8, 28, seed=1)
+    dev = DeviceForest(xf.forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic"), [0])
+    assert np.array_equal(dev.predict(g["X"], OUT_MARGIN), g["margin"])
+    np.testing.assert_allclose(dev.predict(g["X"], OUT_PREDICT), g["prob"], rtol=RTOL)
+    assert np.array_equal(dev.predict(g["X"], OUT_LEAF), g["leaf"])
+    trees3, ti3 = xf.synthetic_complete_trees(30, 6, 28, seed=2, num_class=3)
+    dev3 = DeviceForest(xf.forest_from_raw_trees(trees3, ti3, 28, 3, 0.5, "multi:softprob"), [0])
+    assert np.array_equal(dev3.predict(g["X"], OUT_MARGIN), g["margin3"])
+    np.testing.assert_allclose(dev3.predict(g["X"], OUT_PREDICT), g["prob3"], rtol=RTOL)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lgb_synthetic_golden(golden, tmp_path, dtype):
+    g = np.load(os.path.join(golden, "lgb_synth.npz"))
+    trees = lf.synthetic_leafwise_trees(20, 63, 28, seed=3)
+    p = str(tmp_path / "model.txt")
+    lf.write_lightgbm_text(p, trees, 28, "binary sigmoid:1")
+    dev = DeviceForest(load_lightgbm_model(p), [0])
+    X = g["X"].astype(dtype)
+    if dtype == np.float64:
+        raw, prob, leaf = g["raw"], g["prob"], g["leaf"]
+    else:
+        lm = lgb_ref.read_lgb_text(p)
+        Xd = X.astype(np.float64)
+        raw, prob, leaf = (lgb_ref.predict(lm, Xd, raw_score=True), lgb_ref.predict(lm, Xd),
+                           lgb_ref.leaf_index(lm, Xd))
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), raw)
+    np.testing.assert_allclose(dev.predict(X, OUT_PREDICT), prob, rtol=RTOL)
+    assert np.array_equal(dev.predict(X, OUT_LEAF), leaf)
+
+
+def test_sklearn_goldens_bit_exact(golden):
+    f = load_tree_arrays(os.path.join(golden, "sk_rf_reg_model.npz"))
+    g = np.load(os.path.join(golden, "sk_rf_reg.npz"))
+    dev = DeviceForest(f, [0])
+    assert dev.info()["layout"] == 1          # depth-16 trees: explicit layout
+    assert np.array_equal(dev.predict(g["X"], OUT_PREDICT), g["predict"])
+    assert np.array_equal(dev.predict(g["X"], OUT_LEAF), g["apply"])
+    fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
+    gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
+    devc = DeviceForest(fc, [0])
+    assert np.array_equal(devc.predict(gc["X"], OUT_MARGIN), gc["predict_proba"])
+    lab = fc.meta["classes"].take(devc.predict(gc["X"], OUT_PREDICT).astype(np.int64))
+    assert np.array_equal(lab, gc["predict"])
+
+
+def test_sklearnserver_plugin(golden, tmp_path):
+    import shutil
+    from kfserving_amd.sklearnserver import SKLearnModel
+    shutil.copy(os.path.join(golden, "sk_rf_clf_model.npz"), str(tmp_path / "model.npz"))
+    model = SKLearnModel("m", str(tmp_path))
+    assert model.load()
+    gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
+    X = np.nan_to_num(gc["X"][:64])
+    from oracle import sk_ref
+    from tests.test_oracle import _sk_trees
+    trees, z = _sk_trees(os.path.join(golden, "sk_rf_clf_model.npz"))
+    want = sk_ref.predict_classifier(trees, X, z["classes"]).tolist()
+    assert model.predict({"instances": X.tolist()})["predictions"] == want
+
+
+# ---------------------------------------------------------------- edge cases
+@pytest.fixture(scope="module")
+def c2_small():
+    trees, ti = xf.synthetic_complete_trees(50, 8, 28, seed=21)
+    ref = xgb_ref.from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic")
+    dev = DeviceForest(xf.forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic"), [0])
+    return trees, ti, ref, dev
+
+
+@pytest.mark.parametrize("rows", [0, 1, 63, 255, 256, 257, 1000, 4099])
+def test_ragged_row_counts(c2_small, rows):
+    _, _, ref, dev = c2_small
+    X = np.random.default_rng(rows).standard_normal((rows, 28)).astype(np.float32)
+    got = dev.predict(X, OUT_MARGIN)
+    assert got.shape == (rows,)
+    if rows:
+        assert np.array_equal(got, xgb_ref.predict(ref, X, output_margin=True))
+
+
+def test_specials_nan_inf_zero_denormal(c2_small):
+    _, _, ref, dev = c2_small
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((2000, 28)).astype(np.float32)
+    specials = np.array([np.nan, np.inf, -np.inf, 0.0, -0.0, 1e-45, -1e-45, 1e-38],
+                        dtype=np.float32)
+    mask = rng.random(X.shape) < 0.2
+    X[mask] = specials[rng.integers(0, len(specials), mask.sum())]
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), xgb_ref.predict(ref, X, output_margin=True))
+    assert np.array_equal(dev.predict(X, OUT_LEAF), xgb_ref.leaf_index(ref, X))
+
+
+def test_fewer_columns_read_as_missing(c2_small):
+    _, _, ref, dev = c2_small
+    X = np.random.default_rng(6).standard_normal((300, 20)).astype(np.float32)
+    Xp = np.concatenate([X, np.full((300, 8), np.nan, np.float32)], axis=1)
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), xgb_ref.predict(ref, Xp, output_margin=True))
+
+
+def test_xgb_list_path_zero_is_missing(golden):
+    """xgbserver with a JSON list: 0 -> missing, NaN -> right (DMatrix(list), 0.82)."""
+    from kfserving_amd.xgbserver import XGBoostModel
+    trees, ti = xf.synthetic_complete_trees(20, 6, 8, seed=8)
+    model = XGBoostModel("m", "", 1, booster=xf.forest_from_raw_trees(trees, ti, 8, 0, 0.0,
+                                                                        "binary:logistic"))
+    ref = xgb_ref.from_raw_trees(trees, ti, 8, 0, 0.0, "binary:logistic")
+    rng = np.random.default_rng(9)
+    X = rng.standard_normal((200, 8))
+    X[rng.random(X.shape) < 0.2] = 0.0
+    X[rng.random(X.shape) < 0.1] = np.nan
+    got = np.array(model.predict({"instances": X.tolist()})["predictions"], dtype=np.float32)
+    np.testing.assert_allclose(got, xgb_ref.predict(ref, X.astype(np.float32), missing="csr"),
+                               rtol=RTOL)
+
+
+def test_device_path_with_row_stride(c2_small):
+    torch = pytest.importorskip("torch")
+    _, _, ref, dev = c2_small
+    X = np.random.default_rng(7).standard_normal((777, 32)).astype(np.float32)
+    xt = torch.from_numpy(X).cuda()
+    out = torch.empty(777, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    dev.predict_device(xt.data_ptr(), 0, 777, 28, 32, OUT_MARGIN, out.data_ptr(), 777,
+                       stream=stream)
+    torch.cuda.synchronize()
+    want = xgb_ref.predict(ref, np.ascontiguousarray(X[:, :28]), output_margin=True)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_row_sharding_across_slots(c2_small):
+    trees, ti, ref, _ = c2_small
+    dev2 = DeviceForest(xf.forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic"),
+                        [0, 0])
+    X = np.random.default_rng(8).standard_normal((10001, 28)).astype(np.float32)
+    assert np.array_equal(dev2.predict(X, OUT_MARGIN), xgb_ref.predict(ref, X, output_margin=True))
+
+
+def test_errors_are_loud(c2_small):
+    _, _, _, dev = c2_small
+    with pytest.raises(TreeInferError):
+        dev.predict_device(0, 0, 10, 28, 28, OUT_MARGIN, 0, 10)   # null pointers
+    with pytest.raises(TreeInferError):
+        dev.predict_device(1, 7, 10, 28, 28, OUT_MARGIN, 1, 10)   # bad dtype
+
+
+# ------------------------------------------------------ full-size properties
+def test_c2_full_size_matches_c_port():
+    """BASELINE config C2 at full size: 500 depth-8 trees, 28 features, 1M rows.
+    Every margin bit-exact against the C/OpenMP restatement of xgboost 0.82."""
+    trees, ti = xf.synthetic_complete_trees(500, 8, 28, seed=0)
+    dev = DeviceForest(xf.forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic"), [0])
+    assert dev.info()["layout"] == 0 and dev.info()["depth"] == 8
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((1_000_000, 28), dtype=np.float32)
+    X[rng.random(X.shape, dtype=np.float32) < 0.01] = np.nan
+    got = dev.predict(X, OUT_MARGIN)
+    want = port.xgb_predict(trees, ti, 1, 0.0, 28, X)[:, 0]
+    assert np.array_equal(got, want)
+    prob = dev.predict(X, OUT_PREDICT)
+    np.testing.assert_allclose(prob, 1.0 / (1.0 + np.exp(-want.astype(np.float64))), rtol=RTOL)
+
+
+def test_leafwise_lgb_full_property():
+    """Config C3 shape (1000 trees x 255 leaves, 100 features) on 200k rows:
+    raw scores bit-exact against the C restatement of lightgbm 2.3.1."""
+    trees = lf.synthetic_leafwise_trees(1000, 255, 100, seed=1)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, 100, "binary sigmoid:1")
+        f = load_lightgbm_model(p)
+    dev = DeviceForest(f, [0])
+    X = np.random.default_rng(2).standard_normal((200_000, 100)).astype(np.float32)
+    got = dev.predict(X, OUT_MARGIN)
+    want = port.lgb_predict_raw(trees, 1, 100, X.astype(np.float64))[:, 0]
+    assert np.array_equal(got, want)
