@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -51,8 +52,27 @@ int fail(int code, const std::string& msg) {
 
 constexpr int kMaxHeapDepth = 8;              // deeper forests use the explicit layout
 constexpr size_t kLdsPerCu = 160 * 1024;      // gfx950
-constexpr size_t kLdsTwoPerCu = 80 * 1024;    // budget for 2 workgroups / CU
 constexpr size_t kFeatLdsMax = 64 * 1024;     // feature image budget per workgroup
+
+// Tuning knobs (read once): TI_HEAP_ROWS = rows per heap workgroup,
+// TI_HEAP_LDS_KB = LDS budget per heap workgroup (features + tree stage).
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  return std::atoi(v);
+}
+
+// Rows per tile (= threads per workgroup) for a feature image of F columns
+// of `xs`-byte elements: the largest of 256/128/64 whose [F][R] image fits
+// kFeatLdsMax; 0 when even 64 rows do not fit (features read from HBM).
+// (512-row tiles measured 25 % slower at F = 28: the bigger image leaves
+// room for fewer workgroups per CU.)
+int pick_rows(int F, size_t xs, int want) {
+  if (want > 0) return want;
+  for (int R = 256; R >= 64; R >>= 1)
+    if (static_cast<size_t>(F) * R * xs <= kFeatLdsMax) return R;
+  return 0;
+}
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
@@ -108,6 +128,7 @@ struct ti_forest {
   int32_t layout = 0;   // 0 heap, 1 explicit
   int32_t depth = 0;
   int64_t stride32 = 0, stride64 = 0;
+  int32_t rows32 = 256, rows64 = 256;   // heap: rows per tile of each image (0 = HBM features)
   // host images (kept until upload)
   std::vector<unsigned char> h_heap32, h_heap64;
   std::vector<int32_t> h_heap_leaf_ids;
@@ -216,8 +237,8 @@ int validate(const ti_forest_desc* d, std::vector<int>* depth_out) {
 
 // ------------------------------------------------------------ heap packing
 template <typename XT, typename ACC>
-void pack_heap(const ti_forest_desc* d, int D, int64_t stride, std::vector<unsigned char>* img,
-               std::vector<int32_t>* leaf_ids) {
+void pack_heap(const ti_forest_desc* d, int D, int64_t stride, uint32_t feat_scale,
+               std::vector<unsigned char>* img, std::vector<int32_t>* leaf_ids) {
   using Node = HeapNode<XT>;
   const int NI = (1 << D) - 1, NL = 1 << D, LW = d->leaf_width;
   img->assign(static_cast<size_t>(stride) * d->n_trees, 0);
@@ -253,7 +274,7 @@ void pack_heap(const ti_forest_desc* d, int D, int64_t stride, std::vector<unsig
           nd.thr = static_cast<decltype(nd.thr)>(round_down_f32(d->threshold[g]));
         else
           nd.thr = static_cast<decltype(nd.thr)>(d->threshold[g]);
-        nd.meta = make_meta(d->feature[g], d->flags[g]);
+        nd.meta = make_meta(static_cast<int32_t>(d->feature[g] * feat_scale), d->flags[g]);
         nodes[it.heap] = nd;
         st.push_back(Item{d->left[g], 2 * it.heap + 1, it.level + 1});
         st.push_back(Item{d->right[g], 2 * it.heap + 2, it.level + 1});
@@ -346,39 +367,56 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
 // ----------------------------------------------------------------- launch
 using KernelFn = void (*)(KArgs);
 
-template <typename XT, typename ACC, int KMAX, bool FL>
+template <typename XT, typename ACC, int KMAX, bool FL, bool Z>
 KernelFn pick_kernel(int layout) {
-  if (layout == 0) return ti::heap_predict_kernel<XT, ACC, KMAX, FL>;
-  return ti::explicit_predict_kernel<XT, ACC, KMAX, FL>;
+  if (layout == 0) return ti::heap_predict_kernel<XT, ACC, KMAX, FL, Z>;
+  return ti::explicit_predict_kernel<XT, ACC, KMAX, FL, Z>;
+}
+
+// the LightGBM zero rule exists only for float64-accumulating forests
+template <typename XT, typename ACC, int KMAX, bool FL>
+KernelFn pick_kernel_z(int layout, bool z) {
+  if constexpr (sizeof(ACC) == 8) {
+    if (z) return pick_kernel<XT, ACC, KMAX, FL, true>(layout);
+  }
+  return pick_kernel<XT, ACC, KMAX, FL, false>(layout);
 }
 
 template <typename XT, typename ACC, int KMAX>
-KernelFn pick_kernel_fl(int layout, bool fl) {
-  return fl ? pick_kernel<XT, ACC, KMAX, true>(layout) : pick_kernel<XT, ACC, KMAX, false>(layout);
+KernelFn pick_kernel_fl(int layout, bool fl, bool z) {
+  return fl ? pick_kernel_z<XT, ACC, KMAX, true>(layout, z)
+            : pick_kernel_z<XT, ACC, KMAX, false>(layout, z);
 }
 
 template <typename XT, typename ACC>
-KernelFn pick_kernel_k(int layout, int K, bool fl) {
-  if (K == 1) return pick_kernel_fl<XT, ACC, 1>(layout, fl);
-  if (K <= 4) return pick_kernel_fl<XT, ACC, 4>(layout, fl);
-  return pick_kernel_fl<XT, ACC, 16>(layout, fl);
+KernelFn pick_kernel_k(int layout, int K, bool fl, bool z) {
+  if (K == 1) return pick_kernel_fl<XT, ACC, 1>(layout, fl, z);
+  if (K <= 4) return pick_kernel_fl<XT, ACC, 4>(layout, fl, z);
+  return pick_kernel_fl<XT, ACC, 16>(layout, fl, z);
 }
 
-KernelFn select_kernel(int layout, int xdt, int accum, int K, bool fl) {
-  if (xdt == TI_F32 && accum == TI_F32) return pick_kernel_k<float, float>(layout, K, fl);
-  if (xdt == TI_F32 && accum == TI_F64) return pick_kernel_k<float, double>(layout, K, fl);
-  if (xdt == TI_F64 && accum == TI_F64) return pick_kernel_k<double, double>(layout, K, fl);
-  return pick_kernel_k<double, float>(layout, K, fl);
+KernelFn select_kernel(int layout, int xdt, int accum, int K, bool fl, bool z) {
+  if (xdt == TI_F32 && accum == TI_F32) return pick_kernel_k<float, float>(layout, K, fl, z);
+  if (xdt == TI_F32 && accum == TI_F64) return pick_kernel_k<float, double>(layout, K, fl, z);
+  if (xdt == TI_F64 && accum == TI_F64) return pick_kernel_k<double, double>(layout, K, fl, z);
+  return pick_kernel_k<double, float>(layout, K, fl, z);
 }
 
 std::mutex g_attr_mu;
 std::set<std::pair<int, const void*>> g_attr_done;
 
-int ensure_lds_attr(int device, KernelFn fn, size_t lds) {
-  if (lds <= 64 * 1024) return TI_OK;
+// Once per (device, kernel): the kernels address LDS as offsets from 0, which
+// holds only while they declare no static LDS -- check it, then raise the
+// dynamic-LDS limit to the whole 160 KiB.
+int ensure_lds_attr(int device, KernelFn fn) {
   std::lock_guard<std::mutex> lk(g_attr_mu);
   auto key = std::make_pair(device, reinterpret_cast<const void*>(fn));
   if (g_attr_done.count(key)) return TI_OK;
+  hipFuncAttributes attr;
+  TI_HIP(hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(fn)));
+  if (attr.sharedSizeBytes != 0)
+    return fail(TI_ERR_DEVICE, "kernel declares " + std::to_string(attr.sharedSizeBytes) +
+                                   " B of static LDS; the LDS-address-0 layout is violated");
   TI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsPerCu)));
   g_attr_done.insert(key);
@@ -402,10 +440,17 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
            int64_t stride, int kind, void* out, hipStream_t stream) {
   if (rows <= 0) return TI_OK;
   const size_t xs = dtype_size(xdt);
-  // block size = rows per tile; keep the [F][R] feature image <= 64 KiB
-  int R = 256;
-  while (R > 64 && static_cast<size_t>(f->F) * R * xs > kFeatLdsMax) R >>= 1;
-  bool feat_lds = static_cast<size_t>(f->F) * R * xs <= kFeatLdsMax;
+  // rows per tile = threads per workgroup; the heap images fixed it at create
+  // time (their meta words hold [F][R] byte offsets)
+  int R;
+  if (f->layout == 0) {
+    R = xdt == TI_F64 ? f->rows64 : f->rows32;
+  } else {
+    R = 256;
+    while (R > 64 && static_cast<size_t>(f->F) * R * xs > kFeatLdsMax) R >>= 1;
+    if (static_cast<size_t>(f->F) * R * xs > kFeatLdsMax) R = 0;
+  }
+  const bool feat_lds = R > 0;
   if (!feat_lds) R = 256;
   const size_t feat_bytes = feat_lds ? align16(static_cast<size_t>(f->F) * R * xs) : 0;
 
@@ -423,7 +468,6 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   a.transform = f->transform;
   a.base_first = f->base_first;
   a.lgb_zero_map = f->lgb_zero_map;
-  a.zero_rule = f->zero_rule;
   a.divide = f->divisor != 1.0;
   a.transform_param = f->tparam;
   a.average_divisor = f->divisor;
@@ -431,20 +475,40 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   a.tree_group = d.tree_group;
   a.out = out;
 
-  size_t lds = feat_bytes;
+  size_t lds = feat_bytes + 16;
   if (f->layout == 0) {
     const int64_t stride_b = xdt == TI_F64 ? f->stride64 : f->stride32;
     a.trees = xdt == TI_F64 ? d.heap64 : d.heap32;
     a.tree_stride = stride_b;
     a.heap_leaf_ids = d.heap_leaf_ids;
     a.depth = f->depth;
-    size_t budget = kLdsTwoPerCu > feat_bytes ? kLdsTwoPerCu - feat_bytes : 0;
-    int64_t S = static_cast<int64_t>(budget / stride_b);
-    if (S < 4) S = static_cast<int64_t>((kLdsPerCu - feat_bytes) / stride_b);
-    if (S < 1) return fail(TI_ERR_UNSUPPORTED, "heap tree record does not fit in LDS");
+    // Stage size S (trees): as many trees as keep the workgroups-per-CU count
+    // that the smallest useful stage (kTilp trees) allows -- occupancy is what
+    // hides the LDS latency of the walk (measured: 3 WG/CU beat 2 WG/CU by
+    // 1.7x at F = 28) -- capped by the prefetch registers (kPf x 16 B x R).
+    // TI_HEAP_LDS_KB overrides with a fixed per-workgroup budget.
+    const size_t fixed = feat_bytes + 16;   // feature image + NaN flag word
+    const int64_t cap = static_cast<int64_t>(ti::kPf) * 16 * R / stride_b;
+    auto wgs = [&](int64_t n) { return kLdsPerCu / (fixed + static_cast<size_t>(n * stride_b)); };
+    static const int budget_kb = env_int("TI_HEAP_LDS_KB", 0);
+    int64_t S;
+    if (budget_kb > 0) {
+      const size_t b = static_cast<size_t>(budget_kb) * 1024;
+      S = b > fixed ? static_cast<int64_t>((b - fixed) / stride_b) : 0;
+      if (S >= ti::kTilp) S -= S % ti::kTilp;
+    } else {
+      S = std::min<int64_t>(ti::kTilp, cap);
+      while (S > 1 && fixed + static_cast<size_t>(S * stride_b) > kLdsPerCu) --S;
+      const size_t best = S >= 1 ? wgs(S) : 0;
+      while (S + ti::kTilp <= cap && S + ti::kTilp <= f->T && wgs(S + ti::kTilp) >= best)
+        S += ti::kTilp;
+    }
+    if (S < 1 || fixed + static_cast<size_t>(S * stride_b) > kLdsPerCu)
+      return fail(TI_ERR_UNSUPPORTED, "heap tree record does not fit in LDS");
+    S = std::min<int64_t>(S, cap);
     S = std::min<int64_t>(S, f->T);
     a.stage_trees = static_cast<int32_t>(S);
-    lds = feat_bytes + static_cast<size_t>(S * stride_b);
+    lds = fixed + static_cast<size_t>(S * stride_b);
   } else {
     a.nodes = d.nodes;
     a.thr64 = d.thr64;
@@ -454,9 +518,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.leaves = d.leaves;
     a.exp_leaf_ids = d.exp_leaf_ids;
   }
-  if (lds == 0) lds = 16;
-  KernelFn fn = select_kernel(f->layout, xdt, f->accum, f->K, feat_lds);
-  int rc = ensure_lds_attr(d.device, fn, lds);
+  KernelFn fn = select_kernel(f->layout, xdt, f->accum, f->K, feat_lds, f->zero_rule != 0);
+  int rc = ensure_lds_attr(d.device, fn);
   if (rc) return rc;
   const int64_t grid = (rows + R - 1) / R;
   if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
@@ -550,12 +613,20 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
     f->layout = 0;
     f->stride32 = static_cast<int64_t>(align16(sizeof(HeapNode<float>) * NI + acc_sz * NL * f->LW));
     f->stride64 = static_cast<int64_t>(align16(sizeof(HeapNode<double>) * NI + acc_sz * NL * f->LW));
+    const int want = env_int("TI_HEAP_ROWS", 0);
+    f->rows32 = pick_rows(f->F, 4, want);
+    f->rows64 = pick_rows(f->F, 8, want);
+    // feature byte offset: column of the [F][R] LDS image, or of the row in HBM
+    const uint32_t sc32 = f->rows32 ? static_cast<uint32_t>(f->rows32) * 4u : 4u;
+    const uint32_t sc64 = f->rows64 ? static_cast<uint32_t>(f->rows64) * 8u : 8u;
+    if (static_cast<uint64_t>(f->F) * std::max(sc32, sc64) > ti::kMetaFeatMask)
+      return fail(TI_ERR_UNSUPPORTED, "feature image offsets exceed 24 bits");
     if (f->accum == TI_F64) {
-      pack_heap<float, double>(desc, D, f->stride32, &f->h_heap32, &f->h_heap_leaf_ids);
-      pack_heap<double, double>(desc, D, f->stride64, &f->h_heap64, nullptr);
+      pack_heap<float, double>(desc, D, f->stride32, sc32, &f->h_heap32, &f->h_heap_leaf_ids);
+      pack_heap<double, double>(desc, D, f->stride64, sc64, &f->h_heap64, nullptr);
     } else {
-      pack_heap<float, float>(desc, D, f->stride32, &f->h_heap32, &f->h_heap_leaf_ids);
-      pack_heap<double, float>(desc, D, f->stride64, &f->h_heap64, nullptr);
+      pack_heap<float, float>(desc, D, f->stride32, sc32, &f->h_heap32, &f->h_heap_leaf_ids);
+      pack_heap<double, float>(desc, D, f->stride64, sc64, &f->h_heap64, nullptr);
     }
   } else {
     f->layout = 1;

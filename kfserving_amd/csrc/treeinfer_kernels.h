@@ -1,22 +1,25 @@
 // treeinfer_kernels.h — gfx950 tree-traversal kernels (device code).
 //
-// Two layouts, one row per lane, one 64-wide wavefront walking the SAME tree
-// at a time so tree data is shared across lanes:
+// One row per lane; all 64 lanes of a wavefront walk the SAME tree at a time,
+// so tree data is shared by the whole workgroup.  Two layouts:
 //
 //  * heap  : every tree padded to a complete binary tree of depth D (<= 8).
 //            Children are implicit (2i+1 / 2i+2); a tree is one contiguous
-//            record {internal nodes[2^D-1], leaves[2^D * leaf_width]} and the
-//            workgroup stages S whole records at a time into LDS.  Each lane
-//            walks 4 trees at once (4 independent LDS-latency chains) and adds
-//            the leaves in tree order, so float32 sums are bit-identical to the
-//            library's sequential loop.
+//            record {internal nodes[2^D-1], leaves[2^D * leaf_width]}.  The
+//            workgroup copies S whole records at a time into LDS; each lane
+//            then walks TILP trees at once (TILP independent LDS-latency
+//            chains) and adds their leaves in tree order, so float32 sums are
+//            bit-identical to the library's sequential loop.
 //  * expl  : irregular / deep trees (LightGBM leaf-wise, sklearn depth 16).
 //            Explicit child indices, nodes read from global memory (L2 / MALL
 //            resident), a divergent while-loop per tree.
 //
-// Row features are staged once per 256-row tile into LDS as [feature][row]:
-// lane l reads column f at LDS word f*R + l, so the 64 lanes of a ds_read_b32
-// hit 64 distinct banks whatever feature each lane's node tests.
+// Row features are staged once per tile into LDS as [feature][row]: lane l
+// reads column f at byte f*R*sizeof(XT) + l*sizeof(XT), so the lanes of a
+// ds_read_b32 hit distinct banks whatever feature each lane's node tests.  In
+// the heap layout a node's meta word carries that column byte offset directly
+// (low 24 bits), so the feature address is one v_and_or of meta and the lane
+// offset.
 //
 // The margin epilogue (base, average, sigmoid / softmax / argmax ...) is fused
 // into the same launch: one kernel per predict.
@@ -27,12 +30,22 @@
 
 #include "treeinfer.h"
 
+#ifndef TI_TILP
+#define TI_TILP 8   // trees walked concurrently per lane (heap layout)
+#endif
+#ifndef TI_PF
+#define TI_PF 8     // 16-byte words per thread prefetched for the next tree stage
+#endif
+
 namespace ti {
 
 constexpr uint32_t kMetaNanLeft = 0x80000000u;
 constexpr uint32_t kMetaZeroFlip = 0x40000000u;
 constexpr uint32_t kMetaFeatMask = 0x00FFFFFFu;
 constexpr int kMaxGroups = 16;
+constexpr int kTilp = TI_TILP;
+constexpr int kPf = TI_PF;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
 
 template <typename XT> struct HeapNode;
 template <> struct HeapNode<float> { float thr; uint32_t meta; };                   // 8 B
@@ -54,11 +67,9 @@ struct KArgs {
   int32_t transform;
   int32_t base_first;
   int32_t lgb_zero_map;
-  int32_t zero_rule;
   int32_t divide;
   int32_t depth;          // heap depth D
   int32_t stage_trees;    // heap: trees per LDS stage
-  int32_t pad0;
   double transform_param;
   double average_divisor;
   double base[kMaxGroups];
@@ -98,30 +109,54 @@ __device__ __forceinline__ XT zero_map(XT v, int on) {
   return (on && __builtin_fabs((double)v) <= (double)1e-35f) ? XT(0) : v;
 }
 
-// Canonical split rule (treeinfer.h): left iff x <= thr, NaN by flag,
-// x == 0 flipped for LightGBM Zero-missing nodes whose default differs.
-template <typename XT, typename TT>
-__device__ __forceinline__ bool go_left(XT x, TT thr, uint32_t meta, int zero_rule) {
+// Canonical split rule (treeinfer.h): left iff x <= thr; a NaN goes left iff
+// the node's NaN bit (meta bit 31) is set; with ZERO, x == 0 flips the compare
+// for LightGBM Zero-missing nodes whose default differs (meta bit 30).
+// CHECK_NAN = false is the uniform fast path for tiles known to hold no NaN.
+template <bool ZERO, bool CHECK_NAN = true, typename XT>
+__device__ __forceinline__ bool go_left(XT x, XT thr, uint32_t meta) {
   bool left = x <= thr;
-  const bool nanx = x != x;
-  left = nanx ? ((meta & kMetaNanLeft) != 0) : left;
-  if (zero_rule) {
-    const bool flip = (x == XT(0)) && ((meta & kMetaZeroFlip) != 0);
-    left = flip ? !left : left;
-  }
+  if (CHECK_NAN) left = left || ((x != x) && (int32_t)meta < 0);
+  if (ZERO) left = left != ((x == XT(0)) && (meta & kMetaZeroFlip) != 0);
   return left;
 }
 
-// Stage the tile's features into LDS as [f][R].  Columns >= n_cols read NaN
-// (missing), matching a DMatrix narrower than the booster.
+// One heap node from LDS in a single wide read (ds_read_b64 / ds_read_b128).
+__device__ __forceinline__ void load_node(const HeapNode<float>* p, float& thr, uint32_t& meta) {
+  const uint2 v = *reinterpret_cast<const uint2*>(p);
+  thr = __uint_as_float(v.x);
+  meta = v.y;
+}
+__device__ __forceinline__ void load_node(const HeapNode<double>* p, double& thr, uint32_t& meta) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  thr = __hiloint2double((int)v.y, (int)v.x);
+  meta = v.z;
+}
+
+// The dynamic LDS region starts at LDS address 0 (no static __shared__ in
+// these kernels), so a feature-image byte offset is already an LDS address.
 template <typename XT>
-__device__ __forceinline__ void stage_features(XT* feat, const KArgs& a, int64_t row0, int R, int tid) {
+__device__ __forceinline__ XT lds_at(uint32_t byte_addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) XT*>(
+      static_cast<uintptr_t>(byte_addr));
+}
+
+// Stage the tile's features into LDS as [f][R].  Columns >= n_cols read NaN
+// (missing), matching a DMatrix narrower than the booster.  Returns (uniformly
+// across the workgroup) whether the tile holds a NaN; `flag` is a word of the
+// dynamic LDS region (no static __shared__: see lds_at).  Ends in a barrier.
+template <typename XT>
+__device__ __forceinline__ bool stage_features(XT* feat, volatile int* flag, const KArgs& a,
+                                               int64_t row0, int R, int tid) {
+  if (tid == 0) *flag = 0;
+  __syncthreads();
   const XT* X = static_cast<const XT*>(a.X);
   const int F = a.n_features;
   const int C = a.n_cols;
   const int FC = F < C ? F : C;
   const int64_t left_rows = a.n_rows - row0;
   const int rows_here = left_rows < R ? (int)left_rows : R;
+  bool has_nan = false;
   if (a.row_stride == C) {
     // the tile is one contiguous span: consecutive lanes read consecutive words
     const XT* base = X + row0 * (int64_t)C;
@@ -130,24 +165,25 @@ __device__ __forceinline__ void stage_features(XT* feat, const KArgs& a, int64_t
     for (uint32_t e = tid; e < n; e += R) {
       const uint32_t r = e / uC;
       const uint32_t c = e - r * uC;
-      if ((int)c < F) feat[c * R + r] = zero_map(base[e], a.lgb_zero_map);
+      const XT v = base[e];
+      if ((int)c < F) {
+        feat[c * R + r] = zero_map(v, a.lgb_zero_map);
+        has_nan |= v != v;
+      }
     }
   } else if (tid < rows_here) {
     const XT* xr = X + (row0 + tid) * a.row_stride;
-    for (int c = 0; c < FC; ++c) feat[c * R + tid] = zero_map(xr[c], a.lgb_zero_map);
+    for (int c = 0; c < FC; ++c) {
+      const XT v = xr[c];
+      feat[c * R + tid] = zero_map(v, a.lgb_zero_map);
+      has_nan |= v != v;
+    }
   }
   for (int c = FC; c < F; ++c) feat[c * R + tid] = nan_value<XT>();
-}
-
-// Feature fetch for a lane: LDS image, or straight from the row (very wide F).
-template <typename XT, bool FEAT_LDS>
-__device__ __forceinline__ XT fetch(const XT* feat, const XT* xrow, uint32_t f, int R, int tid,
-                                    const KArgs& a) {
-  if (FEAT_LDS) {
-    return feat[f * R + tid];
-  } else {
-    return (int)f < a.n_cols ? zero_map(xrow[f], a.lgb_zero_map) : nan_value<XT>();
-  }
+  // rows past n_rows stay unwritten: their lanes compute and discard
+  if (has_nan || FC < F) *flag = 1;
+  __syncthreads();
+  return *flag != 0;
 }
 
 template <typename ACC, int KMAX>
@@ -240,80 +276,145 @@ __device__ __forceinline__ void finish_row(const ACC (&acc)[KMAX], const KArgs& 
   }
 }
 
+// Tree stages move global -> registers -> LDS.  The next stage's loads are
+// issued before the current stage is walked and land in registers while the
+// lanes traverse, so only the LDS write sits between two stages.  A stage is
+// at most kPf * 16 * R bytes (the host sizes it so).
+__device__ __forceinline__ void prefetch_stage(u32x4 (&pf)[kPf], const u32x4* __restrict__ src,
+                                               int n16, int tid, int R) {
+  // unconditional loads (index clamped inside the stage): no exec-masked
+  // branches, so every load is in flight at once and pf stays in registers
+#pragma unroll
+  for (int u = 0; u < kPf; ++u) {
+    const int i = tid + u * R;
+    pf[u] = src[i < n16 ? i : n16 - 1];
+  }
+}
+__device__ __forceinline__ void commit_stage(const u32x4 (&pf)[kPf], u32x4* __restrict__ dst,
+                                             int n16, int tid, int R) {
+#pragma unroll
+  for (int u = 0; u < kPf; ++u) {
+    const int i = tid + u * R;
+    if (i < n16) dst[i] = pf[u];
+  }
+}
+
 // ---------------------------------------------------------------- heap kernel
-template <typename XT, typename ACC, int KMAX, bool FEAT_LDS>
-__global__ void __launch_bounds__(256) heap_predict_kernel(const KArgs a) {
+// meta bits 0..23 hold the node's feature as a byte offset: into the LDS
+// feature image (FEAT_LDS) or into the row (global fallback for very wide F).
+template <typename XT, typename ACC, int KMAX, bool FEAT_LDS, bool ZERO, bool CHECK_NAN>
+__device__ __forceinline__ void heap_stage(const KArgs& a, const unsigned char* stage, int cnt,
+                                           int t0, ACC (&acc)[KMAX], uint32_t lane_off,
+                                           const unsigned char* xrow, int64_t row, bool live) {
   using Node = HeapNode<XT>;
+  const int D = a.depth;
+  const int NI = (1 << D) - 1;
+  const int NL = 1 << D;
+  const int T = a.n_trees;
+  const int64_t stride = a.tree_stride;
+  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
+  const uint32_t col_limit = (uint32_t)a.n_cols * (uint32_t)sizeof(XT);
+  for (int j = 0; j < cnt; j += kTilp) {
+    const Node* tp[kTilp];
+#pragma unroll
+    for (int q = 0; q < kTilp; ++q) {
+      const int tq = (j + q) < cnt ? (j + q) : (cnt - 1);
+      tp[q] = reinterpret_cast<const Node*>(stage + (int64_t)tq * stride);
+    }
+    uint32_t idx[kTilp];
+#pragma unroll
+    for (int q = 0; q < kTilp; ++q) idx[q] = 0u;
+    for (int l = 0; l < D; ++l) {
+      XT thr[kTilp];
+      uint32_t meta[kTilp];
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q) load_node(tp[q] + idx[q], thr[q], meta[q]);
+      XT x[kTilp];
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q) {
+        const uint32_t off = meta[q] & kMetaFeatMask;
+        if (FEAT_LDS) {
+          x[q] = lds_at<XT>(off | lane_off);
+        } else {
+          x[q] = off < col_limit ? zero_map(*reinterpret_cast<const XT*>(xrow + off),
+                                            a.lgb_zero_map)
+                                 : nan_value<XT>();
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q)
+        idx[q] = 2u * idx[q] + (go_left<ZERO, CHECK_NAN>(x[q], thr[q], meta[q]) ? 1u : 2u);
+    }
+#pragma unroll
+    for (int q = 0; q < kTilp; ++q) {
+      if (j + q < cnt) {
+        const int leaf = (int)idx[q] - NI;
+        const int t = t0 + j + q;
+        if (want_leaf) {
+          if (live) static_cast<int32_t*>(a.out)[row * T + t] = a.heap_leaf_ids[(int64_t)t * NL + leaf];
+        } else {
+          const ACC* lv = reinterpret_cast<const ACC*>(tp[q] + NI);
+          add_leaf<ACC, KMAX>(acc, lv, leaf, a.leaf_width, a.tree_group[t]);
+        }
+      }
+    }
+  }
+}
+
+template <typename XT, typename ACC, int KMAX, bool FEAT_LDS, bool ZERO>
+__global__ void __launch_bounds__(512) heap_predict_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int R = blockDim.x;
   const int tid = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * R;
   const int64_t row = row0 + tid;
   const bool live = row < a.n_rows;
-  XT* feat = reinterpret_cast<XT*>(smem);
   const size_t feat_bytes = FEAT_LDS ? align16((size_t)a.n_features * R * sizeof(XT)) : 0;
-  unsigned char* stage = smem + feat_bytes;
-  const XT* xrow = static_cast<const XT*>(a.X) + (live ? row : a.n_rows - 1) * a.row_stride;
-  if (FEAT_LDS) stage_features<XT>(feat, a, row0, R, tid);
-
-  const int D = a.depth;
-  const int NI = (1 << D) - 1;
-  const int NL = 1 << D;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + feat_bytes);
+  unsigned char* stage = smem + feat_bytes + 16;
+  const unsigned char* xrow = reinterpret_cast<const unsigned char*>(
+      static_cast<const XT*>(a.X) + (live ? row : a.n_rows - 1) * a.row_stride);
+  const uint32_t lane_off = (uint32_t)tid * (uint32_t)sizeof(XT);
+  // without an LDS image the NaN path is always taken
+  const bool tile_nan =
+      FEAT_LDS ? stage_features<XT>(reinterpret_cast<XT*>(smem), flag, a, row0, R, tid) : true;
   const int T = a.n_trees;
   const int S = a.stage_trees;
   const int64_t stride = a.tree_stride;
-  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
-  int32_t* out_leaf = static_cast<int32_t*>(a.out);
 
   ACC acc[KMAX];
   init_acc(acc, a);
 
+  // stage k covers trees [k*S, min(T, (k+1)*S)); the last stage re-prefetches
+  // itself so the loop body has no conditional register traffic
+  const int last0 = ((T - 1) / S) * S;
+  u32x4 pf[kPf];
+  prefetch_stage(pf, reinterpret_cast<const u32x4*>(a.trees),
+                 (int)(((int64_t)(T < S ? T : S) * stride) >> 4), tid, R);
   for (int t0 = 0; t0 < T; t0 += S) {
     const int cnt = (T - t0) < S ? (T - t0) : S;
-    __syncthreads();   // previous stage fully consumed (and features staged)
-    {
-      const uint4* src = reinterpret_cast<const uint4*>(a.trees + (int64_t)t0 * stride);
-      uint4* dst = reinterpret_cast<uint4*>(stage);
-      const int n16 = (int)(((int64_t)cnt * stride) >> 4);
-      for (int i = tid; i < n16; i += R) dst[i] = src[i];
-    }
+    __syncthreads();   // previous stage fully consumed (first pass: features staged)
+    commit_stage(pf, reinterpret_cast<u32x4*>(stage), (int)(((int64_t)cnt * stride) >> 4), tid, R);
     __syncthreads();
-    for (int j = 0; j < cnt; j += 4) {
-      const unsigned char* tp[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) tp[q] = stage + (int64_t)((j + q) < cnt ? (j + q) : (cnt - 1)) * stride;
-      uint32_t idx[4] = {0u, 0u, 0u, 0u};
-      for (int l = 0; l < D; ++l) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const Node nd = reinterpret_cast<const Node*>(tp[q])[idx[q]];
-          const XT x = fetch<XT, FEAT_LDS>(feat, xrow, nd.meta & kMetaFeatMask, R, tid, a);
-          const bool left = go_left(x, (XT)nd.thr, nd.meta, a.zero_rule);
-          idx[q] = 2u * idx[q] + (left ? 1u : 2u);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (j + q < cnt) {
-          const int leaf = (int)idx[q] - NI;
-          const int t = t0 + j + q;
-          if (want_leaf) {
-            if (live) out_leaf[row * T + t] = a.heap_leaf_ids[(int64_t)t * NL + leaf];
-          } else {
-            const ACC* lv = reinterpret_cast<const ACC*>(tp[q] + (size_t)NI * sizeof(Node));
-            add_leaf<ACC, KMAX>(acc, lv, leaf, a.leaf_width, a.tree_group[t]);
-          }
-        }
-      }
+    {                  // next stage in flight while this one is walked
+      const int tn = t0 + S <= last0 ? t0 + S : last0;
+      const int cn = (T - tn) < S ? (T - tn) : S;
+      prefetch_stage(pf, reinterpret_cast<const u32x4*>(a.trees + (int64_t)tn * stride),
+                     (int)(((int64_t)cn * stride) >> 4), tid, R);
     }
+    if (tile_nan)
+      heap_stage<XT, ACC, KMAX, FEAT_LDS, ZERO, true>(a, stage, cnt, t0, acc, lane_off, xrow, row, live);
+    else
+      heap_stage<XT, ACC, KMAX, FEAT_LDS, ZERO, false>(a, stage, cnt, t0, acc, lane_off, xrow, row, live);
   }
-  if (!live || want_leaf) return;
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
   finish_row<ACC, KMAX>(acc, a, row);
 }
 
 // ------------------------------------------------------------ explicit kernel
-template <typename XT, typename ACC, int KMAX, bool FEAT_LDS>
-__global__ void __launch_bounds__(256) explicit_predict_kernel(const KArgs a) {
+// meta bits 0..23 hold the plain feature index.
+template <typename XT, typename ACC, int KMAX, bool FEAT_LDS, bool ZERO>
+__global__ void __launch_bounds__(512) explicit_predict_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int R = blockDim.x;
   const int tid = threadIdx.x;
@@ -323,8 +424,9 @@ __global__ void __launch_bounds__(256) explicit_predict_kernel(const KArgs a) {
   XT* feat = reinterpret_cast<XT*>(smem);
   const XT* xrow = static_cast<const XT*>(a.X) + (live ? row : a.n_rows - 1) * a.row_stride;
   if (FEAT_LDS) {
-    stage_features<XT>(feat, a, row0, R, tid);
-    __syncthreads();
+    volatile int* flag = reinterpret_cast<volatile int*>(
+        smem + align16((size_t)a.n_features * R * sizeof(XT)));
+    stage_features<XT>(feat, flag, a, row0, R, tid);   // ends in a barrier
   }
   const int T = a.n_trees;
   const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
@@ -340,14 +442,15 @@ __global__ void __launch_bounds__(256) explicit_predict_kernel(const KArgs a) {
     int32_t c = a.root[t];
     while (c >= 0) {
       const ExpNode nd = nodes[c];
-      const XT x = fetch<XT, FEAT_LDS>(feat, xrow, nd.meta & kMetaFeatMask, R, tid, a);
-      bool left;
-      if (sizeof(XT) == 4) {
-        left = go_left(x, (XT)nd.thr, nd.meta, a.zero_rule);
+      const uint32_t f = nd.meta & kMetaFeatMask;
+      XT x;
+      if (FEAT_LDS) {
+        x = feat[f * R + tid];
       } else {
-        left = go_left(x, (XT)a.thr64[nb + c], nd.meta, a.zero_rule);
+        x = (int)f < a.n_cols ? zero_map(xrow[f], a.lgb_zero_map) : nan_value<XT>();
       }
-      c = left ? nd.left : nd.right;
+      const XT thr = sizeof(XT) == 4 ? (XT)nd.thr : (XT)a.thr64[nb + c];
+      c = go_left<ZERO>(x, thr, nd.meta) ? nd.left : nd.right;
     }
     const int64_t lb = a.leaf_base[t];
     if (want_leaf) {

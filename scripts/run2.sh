@@ -1,0 +1,1 @@
+bash scripts/gpu_check.sh && bash scripts/sweep.sh

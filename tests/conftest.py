@@ -8,6 +8,15 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# PyTorch-ROCm bundles its own libamdhip64 (soname libamdhip64.so.7, NEEDED as
+# "libamdhip64.so").  Loading torch first makes libtreeinfer bind to that same
+# runtime; loading libtreeinfer first would put two HIP runtimes in the process
+# and torch would then see no GPU ("One HIP runtime").
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP library)")
