@@ -58,8 +58,20 @@ def build_model():
 
 
 def shard_rows(total_rows: int, rank: int, world: int):
-    """Weak scaling: every rank owns a full batch of `total_rows` rows with its own seed."""
+    """Weak scaling: every rank owns a full batch of `total_rows` rows with its own seed
+    (rows are independent: no data-path collective)."""
     return total_rows, 1000 + rank
+
+
+def max_over_ranks(value: float, device) -> float:
+    """The slowest rank's wall time (the only collective, outside the timed region)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def cpu_baseline(trees, ti, X_host, target_s):
@@ -127,10 +139,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = max_over_ranks(wall, f"cuda:{local_rank}")
     total_rows = rows * world * args.steps
     value = total_rows / wall
 

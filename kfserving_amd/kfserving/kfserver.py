@@ -1,0 +1,367 @@
+"""KFServer -- the v1/v2 model-server front end (mirror of
+python/kfserving/kfserving/kfserver.py:30-196 and handlers/http.py:27-112).
+
+Same CLI flags (--http_port 8080 --grpc_port 8081 --max_buffer_size
+104857600 --workers 1), the same ten routes (kfserver.py:61-87), status codes
+(404 unknown model, 503 not ready, 400 malformed body, 500 predict failure)
+and response bytes: dict bodies are ``json.dumps`` with
+``Content-Type: application/json; charset=UTF-8`` (test_server.py:151-157),
+string bodies ``text/html; charset=UTF-8``, errors tornado's
+``<html><title>CODE: REASON</title>...`` page with the reason in the status line.
+
+tornado is not available here, so the transport is a small asyncio HTTP/1.1
+server (keep-alive, Content-Length and chunked request bodies).  Like
+``HTTPServer.start(workers)`` (kfserver.py:99) it binds first and then forks
+``workers`` processes that share the listening socket; models are loaded
+before the fork and their GPU state is created lazily in each worker.
+A synchronous ``predict`` runs in a worker thread (the GPU call releases the
+GIL) instead of blocking the event loop as the tornado handler does
+(http.py:79); an optional in-process batcher (kfserving_amd.batcher) can be
+put in front of ``:predict``.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import inspect
+import json
+import logging
+import os
+import re
+import socket
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from http import HTTPStatus
+from typing import Dict, List, Optional, Tuple
+
+from .errors import HTTPError
+from .kfmodel_repository import KFModelRepository
+
+DEFAULT_HTTP_PORT = 8080
+DEFAULT_GRPC_PORT = 8081
+DEFAULT_MAX_BUFFER_SIZE = 104857600
+
+parser = argparse.ArgumentParser(add_help=False)
+parser.add_argument('--http_port', default=DEFAULT_HTTP_PORT, type=int,
+                    help='The HTTP Port listened to by the model server.')
+parser.add_argument('--grpc_port', default=DEFAULT_GRPC_PORT, type=int,
+                    help='The GRPC Port listened to by the model server.')
+parser.add_argument('--max_buffer_size', default=DEFAULT_MAX_BUFFER_SIZE, type=int,
+                    help='The max buffer size for tornado.')
+parser.add_argument('--workers', default=1, type=int,
+                    help='The number of works to fork')
+parser.add_argument('--max_batchsize', default=0, type=int,
+                    help='Enable the in-process batcher with this many rows per batch (0 = off).')
+parser.add_argument('--max_latency_ms', default=5000, type=int,
+                    help='Batcher flush latency in milliseconds.')
+args, _ = parser.parse_known_args()
+
+JSON_CT = "application/json; charset=UTF-8"
+HTML_CT = "text/html; charset=UTF-8"
+
+Response = Tuple[int, str, Dict[str, str], bytes]
+
+
+def _json_body(obj) -> bytes:
+    # tornado.escape.json_encode
+    return json.dumps(obj).replace("</", "<\\/").encode("utf-8")
+
+
+def _ok(body, content_type=None) -> Response:
+    if isinstance(body, (dict, list)) and content_type is None:
+        return 200, "OK", {"Content-Type": JSON_CT}, _json_body(body)
+    if isinstance(body, str):
+        return 200, "OK", {"Content-Type": content_type or HTML_CT}, body.encode("utf-8")
+    return 200, "OK", {"Content-Type": content_type or HTML_CT}, bytes(body)
+
+
+def error_response(code: int, reason: str) -> Response:
+    page = "<html><title>%d: %s</title><body>%d: %s</body></html>" % (code, reason, code, reason)
+    return code, reason, {"Content-Type": HTML_CT}, page.encode("utf-8")
+
+
+class Application:
+    """Route table + handlers, independent of the socket transport."""
+
+    def __init__(self, models: KFModelRepository, executor: Optional[ThreadPoolExecutor] = None,
+                 batcher_factory=None):
+        self.models = models
+        self.executor = executor or ThreadPoolExecutor(max_workers=8)
+        self._batchers = {}
+        self._batcher_factory = batcher_factory
+        name = r"([a-zA-Z0-9_-]+)"
+        self.routes = [
+            (re.compile(r"^/$"), self.liveness),
+            (re.compile(r"^/v2/health/live$"), self.liveness),
+            (re.compile(r"^/v1/models$"), self.list_models),
+            (re.compile(r"^/v2/models$"), self.list_models),
+            (re.compile(rf"^/v1/models/{name}$"), self.health),
+            (re.compile(rf"^/v2/models/{name}/status$"), self.health),
+            (re.compile(rf"^/v1/models/{name}:predict$"), self.predict),
+            (re.compile(rf"^/v2/models/{name}/infer$"), self.predict),
+            (re.compile(rf"^/v1/models/{name}:explain$"), self.explain),
+            (re.compile(rf"^/v2/models/{name}/explain$"), self.explain),
+            (re.compile(rf"^/v2/repository/models/{name}/load$"), self.load),
+            (re.compile(rf"^/v2/repository/models/{name}/unload$"), self.unload),
+        ]
+        self._methods = {self.liveness: "GET", self.list_models: "GET", self.health: "GET",
+                         self.predict: "POST", self.explain: "POST", self.load: "POST",
+                         self.unload: "POST"}
+
+    async def handle(self, method: str, path: str, headers: Dict[str, str], body: bytes) -> Response:
+        path = path.split("?", 1)[0]
+        for rx, fn in self.routes:
+            m = rx.match(path)
+            if m is None:
+                continue
+            if method != self._methods[fn]:
+                return error_response(405, "Method Not Allowed")
+            try:
+                return await fn(headers, body, *m.groups())
+            except HTTPError as e:
+                return error_response(e.status_code, e.reason)
+            except Exception as e:   # tornado: uncaught handler exception -> 500
+                logging.exception("request failed: %s", e)
+                return error_response(500, "Internal Server Error")
+        return error_response(404, "Not Found")
+
+    # ------------------------------------------------------------ handlers
+    async def liveness(self, headers, body):
+        return _ok("Alive")
+
+    async def list_models(self, headers, body):
+        return _ok(json.dumps([ob.name for ob in self.models.get_models()]))
+
+    async def health(self, headers, body, name):
+        model = self.models.get_model(name)
+        if model is None:
+            raise HTTPError(404, "Model with name %s does not exist." % name)
+        if not model.ready:
+            raise HTTPError(503, "Model with name %s is not ready." % name)
+        return _ok(json.dumps({"name": model.name, "ready": model.ready}))
+
+    def get_model(self, name: str):
+        model = self.models.get_model(name)
+        if model is None:
+            raise HTTPError(HTTPStatus.NOT_FOUND, "Model with name %s does not exist." % name)
+        if not model.ready:
+            model.load()
+        return model
+
+    @staticmethod
+    def validate(request):
+        if isinstance(request, dict):
+            if ("instances" in request and not isinstance(request["instances"], list)) or \
+               ("inputs" in request and not isinstance(request["inputs"], list)):
+                raise HTTPError(HTTPStatus.BAD_REQUEST,
+                                "Expected \"instances\" or \"inputs\" to be a list")
+        return request
+
+    async def _call(self, fn, request):
+        if inspect.iscoroutinefunction(fn):
+            return await fn(request)
+        return await asyncio.get_running_loop().run_in_executor(self.executor, fn, request)
+
+    async def predict(self, headers, body, name):
+        try:
+            request = json.loads(body)
+        except (json.JSONDecodeError, UnicodeDecodeError) as e:
+            raise HTTPError(HTTPStatus.BAD_REQUEST, "Unrecognized request format: %s" % e)
+        model = self.get_model(name)
+        request = model.preprocess(request)
+        request = self.validate(request)
+        if self._batcher_factory is not None and isinstance(request, dict) \
+                and "instances" in request:
+            batcher = self._batchers.get(name)
+            if batcher is None or batcher.model is not model:
+                batcher = self._batcher_factory(model, self._call)
+                self._batchers[name] = batcher
+            response = await batcher.submit(request["instances"])
+            return _ok(model.postprocess(response))
+        response = await self._call(model.predict, request)
+        response = model.postprocess(response)
+        return _ok(response)
+
+    async def explain(self, headers, body, name):
+        model = self.get_model(name)
+        try:
+            request = json.loads(body)
+        except (json.JSONDecodeError, UnicodeDecodeError) as e:
+            raise HTTPError(HTTPStatus.BAD_REQUEST, "Unrecognized request format: %s" % e)
+        request = model.preprocess(request)
+        request = self.validate(request)
+        response = await self._call(model.explain, request)
+        return _ok(model.postprocess(response))
+
+    async def load(self, headers, body, name):
+        try:
+            fn = self.models.load
+            if inspect.iscoroutinefunction(fn):
+                await fn(name)
+            else:
+                fn(name)
+        except Exception:
+            ex_type, ex_value, _ = sys.exc_info()
+            raise HTTPError(500, f"Model with name {name} is not ready. "
+                                 f"Error type: {ex_type} error msg: {ex_value}")
+        if not self.models.is_model_ready(name):
+            raise HTTPError(503, f"Model with name {name} is not ready.")
+        return _ok(json.dumps({"name": name, "load": True}))
+
+    async def unload(self, headers, body, name):
+        try:
+            self.models.unload(name)
+        except KeyError:
+            raise HTTPError(404, "Model with name %s does not exist." % name)
+        return _ok(json.dumps({"name": name, "unload": True}))
+
+
+class _BodyTooLarge(Exception):
+    pass
+
+
+async def _read_request(reader: asyncio.StreamReader, max_body: int):
+    line = await reader.readline()
+    if not line:
+        return None
+    parts = line.decode("latin-1").rstrip("\r\n").split(" ")
+    if len(parts) != 3:
+        raise ValueError("bad request line")
+    method, target, version = parts
+    headers: Dict[str, str] = {}
+    while True:
+        h = await reader.readline()
+        if h in (b"\r\n", b"\n", b""):
+            break
+        k, _, v = h.decode("latin-1").partition(":")
+        headers[k.strip().lower()] = v.strip()
+    if headers.get("transfer-encoding", "").lower() == "chunked":
+        chunks = []
+        total = 0
+        while True:
+            size = int((await reader.readline()).split(b";")[0].strip() or b"0", 16)
+            if size == 0:
+                await reader.readline()
+                break
+            total += size
+            if total > max_body:
+                raise _BodyTooLarge()
+            chunks.append(await reader.readexactly(size))
+            await reader.readline()
+        body = b"".join(chunks)
+    else:
+        n = int(headers.get("content-length", "0") or 0)
+        if n > max_body:
+            raise _BodyTooLarge()
+        body = await reader.readexactly(n) if n else b""
+    return method, target, version, headers, body
+
+
+def _serialize(resp: Response, keep_alive: bool) -> bytes:
+    code, reason, hdrs, body = resp
+    out = [f"HTTP/1.1 {code} {reason}\r\n"]
+    hdrs = dict(hdrs)
+    hdrs["Content-Length"] = str(len(body))
+    hdrs.setdefault("Server", "kfserving-amd")
+    if not keep_alive:
+        hdrs["Connection"] = "close"
+    for k, v in hdrs.items():
+        out.append(f"{k}: {v}\r\n")
+    out.append("\r\n")
+    return "".join(out).encode("latin-1") + body
+
+
+class KFServer:
+    def __init__(self, http_port: int = args.http_port,
+                 grpc_port: int = args.grpc_port,
+                 max_buffer_size: int = args.max_buffer_size,
+                 workers: int = args.workers,
+                 registered_models: KFModelRepository = None,
+                 max_batchsize: int = args.max_batchsize,
+                 max_latency_ms: int = args.max_latency_ms):
+        self.registered_models = registered_models if registered_models is not None \
+            else KFModelRepository()
+        self.http_port = http_port
+        self.grpc_port = grpc_port
+        self.max_buffer_size = max_buffer_size
+        self.workers = workers
+        self.max_batchsize = max_batchsize
+        self.max_latency_ms = max_latency_ms
+        self._server = None
+        self._sock: Optional[socket.socket] = None
+
+    def create_application(self) -> Application:
+        factory = None
+        if self.max_batchsize and self.max_batchsize > 0:
+            from ..batcher.batcher import ModelBatcher
+            size, lat = self.max_batchsize, self.max_latency_ms
+
+            def factory(model, call):
+                return ModelBatcher(model, call, max_batch_size=size, max_latency_ms=lat)
+        return Application(self.registered_models, batcher_factory=factory)
+
+    def register_model(self, model) -> None:
+        if not model.name:
+            raise Exception("Failed to register model, model.name must be provided.")
+        self.registered_models.update(model)
+        logging.info("Registering model: %s", model.name)
+
+    async def _serve_conn(self, app: Application, reader, writer):
+        try:
+            while True:
+                try:
+                    req = await _read_request(reader, self.max_buffer_size)
+                except _BodyTooLarge:
+                    writer.write(_serialize(error_response(413, "Request Entity Too Large"), False))
+                    await writer.drain()
+                    break
+                except (ValueError, asyncio.IncompleteReadError):
+                    writer.write(_serialize(error_response(400, "Bad Request"), False))
+                    await writer.drain()
+                    break
+                if req is None:
+                    break
+                method, target, version, headers, body = req
+                keep = headers.get("connection", "").lower() != "close" and version == "HTTP/1.1"
+                resp = await app.handle(method, target, headers, body)
+                writer.write(_serialize(resp, keep))
+                await writer.drain()
+                if not keep:
+                    break
+        except (ConnectionResetError, BrokenPipeError):
+            pass
+        finally:
+            try:
+                writer.close()
+            except Exception:
+                pass
+
+    def bind(self, host: str = "0.0.0.0") -> socket.socket:
+        sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        sock.bind((host, self.http_port))
+        sock.listen(1024)
+        sock.setblocking(False)
+        self.http_port = sock.getsockname()[1]
+        self._sock = sock
+        return sock
+
+    async def serve(self, sock: Optional[socket.socket] = None) -> None:
+        """Serve on an already-bound socket until cancelled (used by tests)."""
+        app = self.create_application()
+        sock = sock or self._sock or self.bind()
+        self._server = await asyncio.start_server(
+            lambda r, w: self._serve_conn(app, r, w), sock=sock, limit=2 ** 20)
+        async with self._server:
+            await self._server.serve_forever()
+
+    def start(self, models: List, nest_asyncio: bool = False) -> None:
+        for model in models:
+            self.register_model(model)
+        sock = self.bind()
+        logging.info("Listening on port %s", self.http_port)
+        logging.info("Will fork %d workers", self.workers)
+        for _ in range(max(0, self.workers - 1)):
+            if os.fork() == 0:    # child: serve on the shared socket (GPU is lazily initialised)
+                break
+        asyncio.run(self.serve(sock))

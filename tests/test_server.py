@@ -1,0 +1,206 @@
+"""Server contract tests, modelled on python/kfserving/test/test_server.py:51-236
+(DummyModel echo, liveness, health, exact predict bytes + content type,
+list, load/unload 200/503/404, model-not-ready 503) -- over a real socket."""
+import asyncio
+import http.client
+import json
+import threading
+
+import pytest
+
+from kfserving_amd.kfserving import HTTPError, KFModel, KFModelRepository, KFServer
+
+
+class DummyModel(KFModel):
+    def __init__(self, name):
+        super().__init__(name)
+        self.name = name
+        self.ready = False
+
+    def load(self):
+        self.ready = True
+
+    async def predict(self, request):
+        return {"predictions": request["instances"]}
+
+    async def explain(self, request):
+        return {"predictions": request["instances"]}
+
+
+class SyncModel(KFModel):
+    def __init__(self, name):
+        super().__init__(name)
+        self.ready = True
+        self.calls = 0
+
+    def predict(self, request):
+        self.calls += 1
+        if request["instances"] == ["boom"]:
+            raise Exception("Failed to predict boom")
+        return {"predictions": [[v * 2 for v in row] for row in request["instances"]]}
+
+
+class DummyKFModelRepository(KFModelRepository):
+    def __init__(self, test_load_success):
+        super().__init__(models_dir="/tmp")
+        self.test_load_success = test_load_success
+
+    async def load(self, name):
+        if self.test_load_success:
+            model = DummyModel(name)
+            model.load()
+            self.update(model)
+        return self.test_load_success
+
+
+class _Running:
+    def __init__(self, server):
+        self.server = server
+        self.loop = asyncio.new_event_loop()
+        server.http_port = 0
+        sock = server.bind("127.0.0.1")
+        self.port = server.http_port
+        self.thread = threading.Thread(target=self._run, args=(sock,), daemon=True)
+        self.thread.start()
+
+    def _run(self, sock):
+        asyncio.set_event_loop(self.loop)
+        try:
+            self.loop.run_until_complete(self.server.serve(sock))
+        except asyncio.CancelledError:
+            pass
+
+    def fetch(self, path, method="GET", body=None, headers=None):
+        conn = http.client.HTTPConnection("127.0.0.1", self.port, timeout=30)
+        conn.request(method, path, body=body, headers=headers or {})
+        r = conn.getresponse()
+        data = r.read()
+        conn.close()
+        return r.status, dict(r.getheaders()), data
+
+    def stop(self):
+        for t in asyncio.all_tasks(self.loop):
+            self.loop.call_soon_threadsafe(t.cancel)
+        self.thread.join(timeout=5)
+
+
+@pytest.fixture
+def serve():
+    running = []
+
+    def start(server):
+        r = _Running(server)
+        running.append(r)
+        return r
+    yield start
+    for r in running:
+        r.stop()
+
+
+def test_liveness_model_predict_list(serve):
+    server = KFServer(registered_models=KFModelRepository())
+    model = DummyModel("TestModel")
+    model.load()
+    server.register_model(model)
+    s = serve(server)
+    assert s.fetch("/")[0] == 200 and s.fetch("/")[2] == b"Alive"
+    assert s.fetch("/v2/health/live")[0] == 200
+    assert s.fetch("/v1/models/TestModel")[0] == 200
+    code, hdrs, body = s.fetch("/v1/models/TestModel:predict", "POST", b'{"instances":[[1,2]]}')
+    assert code == 200
+    assert body == b'{"predictions": [[1, 2]]}'                     # test_server.py:156
+    assert hdrs["Content-Type"] == "application/json; charset=UTF-8"  # test_server.py:157
+    code, _, body = s.fetch("/v2/models/TestModel/infer", "POST", b'{"instances":[[1,2]]}')
+    assert code == 200 and body == b'{"predictions": [[1, 2]]}'
+    code, _, body = s.fetch("/v1/models/TestModel:explain", "POST", b'{"instances":[[1,2]]}')
+    assert code == 200 and body == b'{"predictions": [[1, 2]]}'
+    assert s.fetch("/v1/models") == (200, s.fetch("/v1/models")[1], b'["TestModel"]')
+
+
+def test_predict_errors(serve):
+    server = KFServer(registered_models=KFModelRepository())
+    server.register_model(SyncModel("m"))
+    s = serve(server)
+    assert s.fetch("/v1/models/nope:predict", "POST", b'{}')[0] == 404
+    assert s.fetch("/v1/models/m:predict", "POST", b'{not json')[0] == 400
+    assert s.fetch("/v1/models/m:predict", "POST", b'{"instances": 3}')[0] == 400
+    assert s.fetch("/v1/models/m:predict", "POST", b'{"instances": ["boom"]}')[0] == 500
+    code, _, body = s.fetch("/v1/models/m:predict", "POST", b'{"instances": [[1, 2]]}')
+    assert code == 200 and json.loads(body) == {"predictions": [[2, 4]]}
+    assert s.fetch("/v1/models/m:predict", "GET")[0] == 405
+
+
+def test_cloudevent_structured_unwrap(serve):
+    server = KFServer(registered_models=KFModelRepository())
+    m = DummyModel("TestModel")
+    m.load()
+    server.register_model(m)
+    s = serve(server)
+    event = {"specversion": "1.0", "id": "1", "source": "x", "type": "t",
+             "time": "2021-01-01T00:00:00Z", "data": {"instances": [[1, 2]]}}
+    code, _, body = s.fetch("/v1/models/TestModel:predict", "POST", json.dumps(event).encode(),
+                            {"Content-Type": "application/cloudevents+json"})
+    assert code == 200 and body == b'{"predictions": [[1, 2]]}'
+
+
+def test_load_unload(serve):
+    s = serve(KFServer(registered_models=DummyKFModelRepository(test_load_success=True)))
+    code, _, body = s.fetch("/v2/repository/models/model/load", "POST", b"")
+    assert code == 200 and body == b'{"name": "model", "load": true}'
+    code, _, body = s.fetch("/v2/repository/models/model/unload", "POST", b"")
+    assert code == 200 and body == b'{"name": "model", "unload": true}'
+
+
+def test_load_unload_failure(serve):
+    s = serve(KFServer(registered_models=DummyKFModelRepository(test_load_success=False)))
+    assert s.fetch("/v2/repository/models/model/load", "POST", b"")[0] == 503
+    assert s.fetch("/v2/repository/models/model/unload", "POST", b"")[0] == 404
+
+
+def test_model_not_ready(serve):
+    server = KFServer(registered_models=KFModelRepository())
+    server.register_model(DummyModel("TestModel"))
+    s = serve(server)
+    code, _, body = s.fetch("/v1/models/TestModel")
+    assert code == 503 and b"503: Model with name TestModel is not ready." in body
+
+
+def test_keepalive_and_chunked(serve):
+    server = KFServer(registered_models=KFModelRepository())
+    server.register_model(SyncModel("m"))
+    s = serve(server)
+    conn = http.client.HTTPConnection("127.0.0.1", s.port, timeout=30)
+    for i in range(3):
+        conn.request("POST", "/v1/models/m:predict", body=iter([b'{"instances": ', b'[[%d]]}' % i]),
+                     headers={"Transfer-Encoding": "chunked"}, encode_chunked=True)
+        r = conn.getresponse()
+        assert r.status == 200 and json.loads(r.read()) == {"predictions": [[2 * i]]}
+    conn.close()
+
+
+def test_in_process_batcher_route(serve):
+    server = KFServer(registered_models=KFModelRepository(), max_batchsize=8, max_latency_ms=50)
+    model = SyncModel("m")
+    server.register_model(model)
+    s = serve(server)
+    results = []
+
+    def one(i):
+        results.append(s.fetch("/v1/models/m:predict", "POST",
+                               json.dumps({"instances": [[i]]}).encode()))
+    th = [threading.Thread(target=one, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    bodies = [json.loads(b) for c, _, b in results]
+    assert all(c == 200 for c, _, _ in results)
+    assert len({b["batchId"] for b in bodies}) < 8          # requests shared batches
+    for b in bodies:
+        assert b["message"] == "" and len(b["predictions"]) == 1
+    assert sorted(b["predictions"][0][0] for b in bodies) == [2 * i for i in range(8)]
+
+
+def test_httperror_reason():
+    e = HTTPError(404, "x")
+    assert e.status_code == 404 and e.reason == "x"
