@@ -109,6 +109,13 @@ struct DeviceForest {
   void* leaves = nullptr;
   int32_t* exp_leaf_ids = nullptr;
   int32_t* tree_group = nullptr;
+  // compact layout
+  unsigned char* cpt_img[2] = {nullptr, nullptr};
+  int64_t* cpt_off[2] = {nullptr, nullptr};
+  int32_t* cpt_stage[2] = {nullptr, nullptr};
+  int32_t* cpt_nint = nullptr;
+  int32_t* cpt_depth = nullptr;
+  int32_t* cpt_root = nullptr;
   // ti_predict scratch
   void* x_buf = nullptr;
   size_t x_cap = 0;
@@ -129,6 +136,16 @@ struct ti_forest {
   int32_t depth = 0;
   int64_t stride32 = 0, stride64 = 0;
   int32_t rows32 = 256, rows64 = 256;   // heap: rows per tile of each image (0 = HBM features)
+  // compact layout (2): one image per input dtype
+  struct CptImage {
+    std::vector<unsigned char> img;
+    std::vector<int64_t> off;           // [T+1]
+    std::vector<int32_t> stage_start;   // [n_stages+1]
+    int32_t rows = 256;
+    int32_t feat_lds = 1;
+    int64_t max_stage_bytes = 0;
+  } cpt[2];
+  std::vector<int32_t> h_cpt_nint, h_cpt_depth, h_cpt_root;
   // host images (kept until upload)
   std::vector<unsigned char> h_heap32, h_heap64;
   std::vector<int32_t> h_heap_leaf_ids;
@@ -157,7 +174,9 @@ void free_device(DeviceForest& d) {
   if (d.device < 0) return;
   (void)hipSetDevice(d.device);
   void* ptrs[] = {d.heap32, d.heap64, d.heap_leaf_ids, d.nodes, d.thr64, d.node_base, d.root,
-                  d.leaf_base, d.leaves, d.exp_leaf_ids, d.tree_group, d.x_buf, d.out_buf};
+                  d.leaf_base, d.leaves, d.exp_leaf_ids, d.tree_group, d.x_buf, d.out_buf,
+                  d.cpt_img[0], d.cpt_img[1], d.cpt_off[0], d.cpt_off[1], d.cpt_stage[0],
+                  d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -167,6 +186,12 @@ void free_device(DeviceForest& d) {
   d.thr64 = nullptr;
   d.node_base = d.leaf_base = nullptr;
   d.leaves = d.x_buf = d.out_buf = nullptr;
+  for (int i = 0; i < 2; ++i) {
+    d.cpt_img[i] = nullptr;
+    d.cpt_off[i] = nullptr;
+    d.cpt_stage[i] = nullptr;
+  }
+  d.cpt_nint = d.cpt_depth = d.cpt_root = nullptr;
   d.x_cap = d.out_cap = 0;
   d.stream = nullptr;
   d.device = -1;
@@ -285,7 +310,7 @@ void pack_heap(const ti_forest_desc* d, int D, int64_t stride, uint32_t feat_sca
 
 // -------------------------------------------------------- explicit packing
 template <typename ACC>
-void pack_explicit(const ti_forest_desc* d, ti_forest* f) {
+void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
   const int LW = d->leaf_width;
   f->h_nodes.clear();
   f->h_thr64.clear();
@@ -313,7 +338,8 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f) {
       if (d->feature[g] < 0) {
         remap[v] = ~n_leaf++;
         f->h_exp_leaf_ids.push_back(d->leaf_id[g]);
-        for (int k = 0; k < LW; ++k) leaves.push_back(static_cast<ACC>(d->leaf_value[g * LW + k]));
+        if (!leaf_ids_only)
+          for (int k = 0; k < LW; ++k) leaves.push_back(static_cast<ACC>(d->leaf_value[g * LW + k]));
       } else {
         remap[v] = n_int++;
         queue.push_back(d->left[g]);
@@ -336,8 +362,125 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f) {
     }
     f->h_root[t] = remap[0];
   }
+  if (leaf_ids_only) {
+    f->h_nodes.clear();
+    f->h_thr64.clear();
+    f->h_node_base.clear();
+    f->h_root.clear();
+    return;
+  }
   f->h_leaves.resize(leaves.size() * sizeof(ACC));
   if (!leaves.empty()) std::memcpy(f->h_leaves.data(), leaves.data(), f->h_leaves.size());
+}
+
+// ---------------------------------------------------------- compact packing
+// Trees with <= 512 internal nodes and <= 512 leaves, numbered breadth-first
+// like pack_explicit (so leaf ids / leaf_base are shared with it).  Returns
+// false when some tree does not fit the 10-bit child codes.
+constexpr int kCptMaxNodes = 512;
+
+bool compact_fits(const ti_forest_desc* d) {
+  if (d->n_features > 1024) return false;
+  for (int t = 0; t < d->n_trees; ++t) {
+    const int64_t b = d->tree_offset[t], e = d->tree_offset[t + 1];
+    int64_t n_int = 0;
+    for (int64_t g = b; g < e; ++g) n_int += d->feature[g] >= 0;
+    if (n_int > kCptMaxNodes || (e - b) - n_int > kCptMaxNodes) return false;
+  }
+  return true;
+}
+
+template <typename XT, typename ACC>
+void pack_compact(const ti_forest_desc* d, std::vector<unsigned char>* img, std::vector<int64_t>* off,
+                  std::vector<int32_t>* nint, std::vector<int32_t>* root) {
+  using Node = HeapNode<XT>;
+  const int LW = d->leaf_width;
+  off->assign(d->n_trees + 1, 0);
+  nint->assign(d->n_trees, 0);
+  root->assign(d->n_trees, 0);
+  img->clear();
+  std::vector<int32_t> queue, code;
+  for (int t = 0; t < d->n_trees; ++t) {
+    const int64_t b = d->tree_offset[t];
+    const int32_t n = static_cast<int32_t>(d->tree_offset[t + 1] - b);
+    code.assign(n, 0);
+    queue.assign(1, 0);
+    int32_t n_int = 0, n_leaf = 0;
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+      const int32_t v = queue[qi];
+      const int64_t g = b + v;
+      if (d->feature[g] < 0) {
+        code[v] = static_cast<int32_t>(ti::kCptLeaf) + n_leaf++;
+      } else {
+        code[v] = n_int++;
+        queue.push_back(d->left[g]);
+        queue.push_back(d->right[g]);
+      }
+    }
+    const size_t rec = align16(sizeof(Node) * n_int + sizeof(ACC) * n_leaf * LW);
+    const size_t base = img->size();
+    img->resize(base + rec, 0);
+    Node* nodes = reinterpret_cast<Node*>(img->data() + base);
+    ACC* leaves = reinterpret_cast<ACC*>(img->data() + base + sizeof(Node) * n_int);
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+      const int32_t v = queue[qi];
+      const int64_t g = b + v;
+      if (d->feature[g] < 0) {
+        const int32_t j = code[v] - static_cast<int32_t>(ti::kCptLeaf);
+        for (int k = 0; k < LW; ++k) leaves[j * LW + k] = static_cast<ACC>(d->leaf_value[g * LW + k]);
+        continue;
+      }
+      Node nd{};
+      nd.thr = sizeof(XT) == 4 ? static_cast<decltype(nd.thr)>(round_down_f32(d->threshold[g]))
+                               : static_cast<decltype(nd.thr)>(d->threshold[g]);
+      uint32_t w = static_cast<uint32_t>(d->feature[g]) |
+                   (static_cast<uint32_t>(code[d->left[g]]) << 10) |
+                   (static_cast<uint32_t>(code[d->right[g]]) << 20);
+      if (d->flags[g] & TI_NODE_ZERO_FLIP) w |= ti::kMetaZeroFlip;
+      if (d->flags[g] & TI_NODE_NAN_LEFT) w |= ti::kMetaNanLeft;
+      nd.meta = w;
+      nodes[code[v]] = nd;
+    }
+    (*nint)[t] = n_int;
+    (*root)[t] = code[0];
+    (*off)[t + 1] = static_cast<int64_t>(img->size());
+  }
+}
+
+// Feature mode, rows per tile and LDS stages of one compact image.  Returns
+// false if a single tree record cannot be staged.
+bool plan_compact(ti_forest* f, int idx, size_t xs) {
+  ti_forest::CptImage& ci = f->cpt[idx];
+  const int mode = env_int("TI_CPT_FEAT_LDS", -1);   // -1 auto, 0 HBM rows, 1 LDS image
+  const bool lds = mode >= 0 ? mode == 1
+                             : static_cast<size_t>(f->F) * 256 * xs <= static_cast<size_t>(40 * 1024);
+  ci.feat_lds = lds ? 1 : 0;
+  ci.rows = lds ? pick_rows(f->F, xs, 0) : 256;
+  if (ci.rows == 0) {
+    ci.feat_lds = 0;
+    ci.rows = 256;
+  }
+  const size_t fixed = (ci.feat_lds ? align16(static_cast<size_t>(f->F) * ci.rows * xs) : 0) + 16;
+  int64_t max_rec = 0;
+  for (int t = 0; t < f->T; ++t) max_rec = std::max(max_rec, ci.off[t + 1] - ci.off[t]);
+  const int64_t pf_cap = static_cast<int64_t>(ti::kPf) * 16 * ci.rows;
+  const int64_t min_stage = max_rec * std::min<int64_t>(ti::kTilp, f->T);
+  size_t n_wg = kLdsPerCu / (fixed + static_cast<size_t>(std::min(min_stage, pf_cap)));
+  if (n_wg < 1) n_wg = 1;
+  int64_t budget = static_cast<int64_t>(kLdsPerCu / n_wg) - static_cast<int64_t>(fixed);
+  budget = std::min(budget, pf_cap);
+  if (budget < max_rec) return false;
+  ci.stage_start.assign(1, 0);
+  ci.max_stage_bytes = 0;
+  int t0 = 0;
+  while (t0 < f->T) {
+    int t1 = t0 + 1;
+    while (t1 < f->T && ci.off[t1 + 1] - ci.off[t0] <= budget) ++t1;
+    ci.stage_start.push_back(t1);
+    ci.max_stage_bytes = std::max(ci.max_stage_bytes, ci.off[t1] - ci.off[t0]);
+    t0 = t1;
+  }
+  return true;
 }
 
 int upload_device(ti_forest* f, DeviceForest& d, int device) {
@@ -350,6 +493,17 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
     if ((rc = upload(&d.heap32, f->h_heap32, &d.bytes))) return rc;
     if ((rc = upload(&d.heap64, f->h_heap64, &d.bytes))) return rc;
     if ((rc = upload(&d.heap_leaf_ids, f->h_heap_leaf_ids, &d.bytes))) return rc;
+  } else if (f->layout == 2) {
+    for (int i = 0; i < 2; ++i) {
+      if ((rc = upload(&d.cpt_img[i], f->cpt[i].img, &d.bytes))) return rc;
+      if ((rc = upload(&d.cpt_off[i], f->cpt[i].off, &d.bytes))) return rc;
+      if ((rc = upload(&d.cpt_stage[i], f->cpt[i].stage_start, &d.bytes))) return rc;
+    }
+    if ((rc = upload(&d.cpt_nint, f->h_cpt_nint, &d.bytes))) return rc;
+    if ((rc = upload(&d.cpt_depth, f->h_cpt_depth, &d.bytes))) return rc;
+    if ((rc = upload(&d.cpt_root, f->h_cpt_root, &d.bytes))) return rc;
+    if ((rc = upload(&d.leaf_base, f->h_leaf_base, &d.bytes))) return rc;
+    if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
   } else {
     if ((rc = upload(&d.nodes, f->h_nodes, &d.bytes))) return rc;
     if ((rc = upload(&d.thr64, f->h_thr64, &d.bytes))) return rc;
@@ -370,6 +524,7 @@ using KernelFn = void (*)(KArgs);
 template <typename XT, typename ACC, int KMAX, bool FL, bool Z>
 KernelFn pick_kernel(int layout) {
   if (layout == 0) return ti::heap_predict_kernel<XT, ACC, KMAX, FL, Z>;
+  if (layout == 2) return ti::compact_predict_kernel<XT, ACC, KMAX, FL, Z>;
   return ti::explicit_predict_kernel<XT, ACC, KMAX, FL, Z>;
 }
 
@@ -445,6 +600,9 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   int R;
   if (f->layout == 0) {
     R = xdt == TI_F64 ? f->rows64 : f->rows32;
+  } else if (f->layout == 2) {
+    const ti_forest::CptImage& ci = f->cpt[xdt == TI_F64 ? 1 : 0];
+    R = ci.feat_lds ? ci.rows : 0;
   } else {
     R = 256;
     while (R > 64 && static_cast<size_t>(f->F) * R * xs > kFeatLdsMax) R >>= 1;
@@ -509,6 +667,22 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     S = std::min<int64_t>(S, f->T);
     a.stage_trees = static_cast<int32_t>(S);
     lds = fixed + static_cast<size_t>(S * stride_b);
+  } else if (f->layout == 2) {
+    const int ii = xdt == TI_F64 ? 1 : 0;
+    const ti_forest::CptImage& ci = f->cpt[ii];
+    a.trees = d.cpt_img[ii];
+    a.cpt_off = d.cpt_off[ii];
+    a.stage_start = d.cpt_stage[ii];
+    a.n_stages = static_cast<int32_t>(ci.stage_start.size() - 1);
+    a.cpt_nint = d.cpt_nint;
+    a.cpt_depth = d.cpt_depth;
+    a.cpt_root = d.cpt_root;
+    a.leaf_base = d.leaf_base;
+    a.exp_leaf_ids = d.exp_leaf_ids;
+    int sh = 0;
+    while ((static_cast<size_t>(1) << sh) < static_cast<size_t>(R) * xs) ++sh;
+    a.feat_shift = sh;
+    lds = feat_bytes + 16 + static_cast<size_t>(ci.max_stage_bytes);
   } else {
     a.nodes = d.nodes;
     a.thr64 = d.thr64;
@@ -608,7 +782,35 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
 
   const size_t acc_sz = f->accum == TI_F64 ? 8 : 4;
   const int D = f->depth;
-  if (D <= kMaxHeapDepth) {
+  // layout: heap for depth <= 8, compact (LDS-staged) for small irregular
+  // trees, explicit (nodes in HBM) otherwise; TI_FORCE_LAYOUT=heap|compact|
+  // explicit overrides (tests run every layout on the same forest)
+  const char* force = std::getenv("TI_FORCE_LAYOUT");
+  std::string want = force ? force : "";
+  bool use_heap = D <= kMaxHeapDepth;
+  // compact pays only while the [F][256] feature image leaves LDS for tree
+  // stages (measured at F = 100: explicit 19.1 ms, compact 29.6 ms with the
+  // image in LDS, 160 ms reading rows from HBM per visit)
+  bool use_compact = !use_heap && compact_fits(desc) &&
+                     static_cast<size_t>(desc->n_features) * 256 * 4 <= static_cast<size_t>(40 * 1024);
+  if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
+  if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
+  if (want == "explicit") { use_heap = false; use_compact = false; }
+  if (use_compact) {
+    f->h_cpt_depth.assign(depth.begin(), depth.end());
+    if (f->accum == TI_F64) {
+      pack_compact<float, double>(desc, &f->cpt[0].img, &f->cpt[0].off, &f->h_cpt_nint, &f->h_cpt_root);
+      pack_compact<double, double>(desc, &f->cpt[1].img, &f->cpt[1].off, &f->h_cpt_nint, &f->h_cpt_root);
+    } else {
+      pack_compact<float, float>(desc, &f->cpt[0].img, &f->cpt[0].off, &f->h_cpt_nint, &f->h_cpt_root);
+      pack_compact<double, float>(desc, &f->cpt[1].img, &f->cpt[1].off, &f->h_cpt_nint, &f->h_cpt_root);
+    }
+    if (!plan_compact(f.get(), 0, 4) || !plan_compact(f.get(), 1, 8)) use_compact = false;
+  }
+  if (use_compact) {
+    f->layout = 2;
+    pack_explicit<char>(desc, f.get(), /*leaf_ids_only=*/true);
+  } else if (use_heap) {
     const int NI = (1 << D) - 1, NL = 1 << D;
     f->layout = 0;
     f->stride32 = static_cast<int64_t>(align16(sizeof(HeapNode<float>) * NI + acc_sz * NL * f->LW));
@@ -631,9 +833,9 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   } else {
     f->layout = 1;
     if (f->accum == TI_F64)
-      pack_explicit<double>(desc, f.get());
+      pack_explicit<double>(desc, f.get(), false);
     else
-      pack_explicit<float>(desc, f.get());
+      pack_explicit<float>(desc, f.get(), false);
   }
   for (int i = 0; i < n_devices; ++i) {
     f->devs.emplace_back(new DeviceForest());
@@ -650,6 +852,10 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   f->h_nodes.clear(); f->h_nodes.shrink_to_fit();
   f->h_thr64.clear(); f->h_thr64.shrink_to_fit();
   f->h_leaves.clear(); f->h_leaves.shrink_to_fit();
+  for (auto& ci : f->cpt) {
+    ci.img.clear();
+    ci.img.shrink_to_fit();
+  }
   *out = f.release();
   return TI_OK;
 }

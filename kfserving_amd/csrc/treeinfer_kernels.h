@@ -43,6 +43,8 @@ constexpr uint32_t kMetaNanLeft = 0x80000000u;
 constexpr uint32_t kMetaZeroFlip = 0x40000000u;
 constexpr uint32_t kMetaFeatMask = 0x00FFFFFFu;
 constexpr int kMaxGroups = 16;
+constexpr uint32_t kCptLeaf = 512u;       // compact child code >= 512: leaf (code - 512)
+constexpr int kExpIlp = 4;                // trees per lane in the global explicit kernel
 constexpr int kTilp = TI_TILP;
 constexpr int kPf = TI_PF;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
@@ -85,6 +87,14 @@ struct KArgs {
   const int64_t* leaf_base;       // [T]
   const void* leaves;             // [n_leaves * leaf_width] ACC
   const int32_t* exp_leaf_ids;    // [n_leaves]
+  // compact layout (LDS-staged irregular trees)
+  const int64_t* cpt_off;         // [T+1] byte offset of each tree record in the image
+  const int32_t* cpt_nint;        // [T] internal nodes per tree
+  const int32_t* cpt_depth;       // [T] max depth per tree
+  const int32_t* cpt_root;        // [T] root child code (0, or kCptLeaf for a single leaf)
+  const int32_t* stage_start;     // [n_stages+1] first tree of each LDS stage
+  int32_t n_stages;
+  int32_t feat_shift;             // log2(R * sizeof(XT)): column stride of the LDS image
   // shared
   const int32_t* tree_group;      // [T]
   void* out;
@@ -411,8 +421,131 @@ __global__ void __launch_bounds__(512) heap_predict_kernel(const KArgs a) {
   finish_row<ACC, KMAX>(acc, a, row);
 }
 
+// ------------------------------------------------------------ compact kernel
+// Irregular trees with <= 512 internal nodes and <= 512 leaves (LightGBM
+// leaf-wise).  A tree record is {internal nodes[n_int], leaves[n_leaf * LW]};
+// a node is {thr, w}: w bits 0..9 feature, 10..19 left code, 20..29 right
+// code (code < 512: internal node, >= 512: leaf code-512), bit 30 zero flip,
+// bit 31 NaN-left.  Records are staged into LDS like the heap layout; each lane
+// walks kTilp trees for max-depth-of-group steps (a lane that reached a leaf
+// keeps its code), leaving early once every lane of the wave is at a leaf.
+template <typename XT, typename ACC, int KMAX, bool FEAT_LDS, bool ZERO, bool CHECK_NAN>
+__device__ __forceinline__ void compact_stage(const KArgs& a, const unsigned char* stage,
+                                              int64_t stage_base, int t0, int cnt,
+                                              ACC (&acc)[KMAX], uint32_t lane_off,
+                                              const unsigned char* xrow, int64_t row, bool live) {
+  using Node = HeapNode<XT>;
+  const int T = a.n_trees;
+  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
+  const uint32_t col_limit = (uint32_t)a.n_cols;
+  for (int j = 0; j < cnt; j += kTilp) {
+    const Node* tp[kTilp];
+    uint32_t code[kTilp];
+    int dmax = 0;
+#pragma unroll
+    for (int q = 0; q < kTilp; ++q) {
+      const int tq = t0 + ((j + q) < cnt ? (j + q) : (cnt - 1));
+      tp[q] = reinterpret_cast<const Node*>(stage + (a.cpt_off[tq] - stage_base));
+      code[q] = (uint32_t)a.cpt_root[tq];
+      const int d = a.cpt_depth[tq];
+      dmax = d > dmax ? d : dmax;
+    }
+    for (int l = 0; l < dmax; ++l) {
+      XT thr[kTilp];
+      uint32_t w[kTilp];
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q) load_node(tp[q] + (code[q] & (kCptLeaf - 1u)), thr[q], w[q]);
+      XT x[kTilp];
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q) {
+        const uint32_t f = w[q] & 0x3FFu;
+        if (FEAT_LDS) {
+          x[q] = lds_at<XT>((f << a.feat_shift) | lane_off);
+        } else {
+          x[q] = f < col_limit ? zero_map(reinterpret_cast<const XT*>(xrow)[f], a.lgb_zero_map)
+                               : nan_value<XT>();
+        }
+      }
+      bool active = false;
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q) {
+        const bool left = go_left<ZERO, CHECK_NAN>(x[q], thr[q], w[q]);
+        const uint32_t child = (w[q] >> (left ? 10u : 20u)) & 0x3FFu;
+        code[q] = code[q] >= kCptLeaf ? code[q] : child;
+        active |= code[q] < kCptLeaf;
+      }
+      if (__ballot(active) == 0) break;   // wave-uniform early exit
+    }
+#pragma unroll
+    for (int q = 0; q < kTilp; ++q) {
+      if (j + q < cnt) {
+        const int t = t0 + j + q;
+        const int leaf = (int)(code[q] - kCptLeaf);
+        if (want_leaf) {
+          if (live) static_cast<int32_t*>(a.out)[row * T + t] = a.exp_leaf_ids[a.leaf_base[t] + leaf];
+        } else {
+          const ACC* lv = reinterpret_cast<const ACC*>(tp[q] + a.cpt_nint[t]);
+          add_leaf<ACC, KMAX>(acc, lv, leaf, a.leaf_width, a.tree_group[t]);
+        }
+      }
+    }
+  }
+}
+
+template <typename XT, typename ACC, int KMAX, bool FEAT_LDS, bool ZERO>
+__global__ void __launch_bounds__(512) compact_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  const size_t feat_bytes = FEAT_LDS ? align16((size_t)a.n_features * R * sizeof(XT)) : 0;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + feat_bytes);
+  unsigned char* stage = smem + feat_bytes + 16;
+  const unsigned char* xrow = reinterpret_cast<const unsigned char*>(
+      static_cast<const XT*>(a.X) + (live ? row : a.n_rows - 1) * a.row_stride);
+  const uint32_t lane_off = (uint32_t)tid * (uint32_t)sizeof(XT);
+  const bool tile_nan =
+      FEAT_LDS ? stage_features<XT>(reinterpret_cast<XT*>(smem), flag, a, row0, R, tid) : true;
+
+  ACC acc[KMAX];
+  init_acc(acc, a);
+
+  const int NS = a.n_stages;
+  auto words = [&](int s) {
+    return (int)((a.cpt_off[a.stage_start[s + 1]] - a.cpt_off[a.stage_start[s]]) >> 4);
+  };
+  u32x4 pf[kPf];
+  prefetch_stage(pf, reinterpret_cast<const u32x4*>(a.trees), words(0), tid, R);
+  for (int s = 0; s < NS; ++s) {
+    const int t0 = a.stage_start[s];
+    const int cnt = a.stage_start[s + 1] - t0;
+    const int64_t base = a.cpt_off[t0];
+    __syncthreads();
+    commit_stage(pf, reinterpret_cast<u32x4*>(stage), words(s), tid, R);
+    __syncthreads();
+    {
+      const int sn = s + 1 < NS ? s + 1 : s;
+      prefetch_stage(pf, reinterpret_cast<const u32x4*>(a.trees + a.cpt_off[a.stage_start[sn]]),
+                     words(sn), tid, R);
+    }
+    if (tile_nan)
+      compact_stage<XT, ACC, KMAX, FEAT_LDS, ZERO, true>(a, stage, base, t0, cnt, acc, lane_off,
+                                                         xrow, row, live);
+    else
+      compact_stage<XT, ACC, KMAX, FEAT_LDS, ZERO, false>(a, stage, base, t0, cnt, acc, lane_off,
+                                                          xrow, row, live);
+  }
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
 // ------------------------------------------------------------ explicit kernel
-// meta bits 0..23 hold the plain feature index.
+// Any tree shape; nodes stay in global memory (L2 / MALL).  meta bits 0..23
+// hold the plain feature index.  Each lane walks kExpIlp trees at once with
+// unconditional (clamped) node loads so the dependent L2 round trips of the
+// trees overlap; finished trees keep their leaf code.
 template <typename XT, typename ACC, int KMAX, bool FEAT_LDS, bool ZERO>
 __global__ void __launch_bounds__(512) explicit_predict_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -436,27 +569,53 @@ __global__ void __launch_bounds__(512) explicit_predict_kernel(const KArgs a) {
   ACC acc[KMAX];
   init_acc(acc, a);
 
-  for (int t = 0; t < T; ++t) {
-    const int64_t nb = a.node_base[t];
-    const ExpNode* nodes = a.nodes + nb;
-    int32_t c = a.root[t];
-    while (c >= 0) {
-      const ExpNode nd = nodes[c];
-      const uint32_t f = nd.meta & kMetaFeatMask;
-      XT x;
-      if (FEAT_LDS) {
-        x = feat[f * R + tid];
-      } else {
-        x = (int)f < a.n_cols ? zero_map(xrow[f], a.lgb_zero_map) : nan_value<XT>();
-      }
-      const XT thr = sizeof(XT) == 4 ? (XT)nd.thr : (XT)a.thr64[nb + c];
-      c = go_left<ZERO>(x, thr, nd.meta) ? nd.left : nd.right;
+  for (int t0 = 0; t0 < T; t0 += kExpIlp) {
+    int64_t nb[kExpIlp];
+    int32_t c[kExpIlp];
+#pragma unroll
+    for (int q = 0; q < kExpIlp; ++q) {
+      const int tq = (t0 + q) < T ? (t0 + q) : (T - 1);
+      nb[q] = a.node_base[tq];
+      c[q] = a.root[tq];
     }
-    const int64_t lb = a.leaf_base[t];
-    if (want_leaf) {
-      if (live) out_leaf[row * T + t] = a.exp_leaf_ids[lb + (~c)];
-    } else {
-      add_leaf<ACC, KMAX>(acc, leaves + lb * a.leaf_width, ~c, a.leaf_width, a.tree_group[t]);
+    for (;;) {
+      u32x4 nd[kExpIlp];   // {thr32 bits, meta, left, right}; native vector stays in VGPRs
+#pragma unroll
+      for (int q = 0; q < kExpIlp; ++q)
+        nd[q] = *reinterpret_cast<const u32x4*>(a.nodes + nb[q] + (c[q] < 0 ? 0 : c[q]));
+      XT thr[kExpIlp];
+#pragma unroll
+      for (int q = 0; q < kExpIlp; ++q)
+        thr[q] = sizeof(XT) == 4 ? (XT)__uint_as_float(nd[q].x)
+                                 : (XT)a.thr64[nb[q] + (c[q] < 0 ? 0 : c[q])];
+      bool active = false;
+#pragma unroll
+      for (int q = 0; q < kExpIlp; ++q) {
+        const uint32_t f = nd[q].y & kMetaFeatMask;
+        XT x;
+        if (FEAT_LDS) {
+          x = feat[f * R + tid];
+        } else {
+          x = (int)f < a.n_cols ? zero_map(xrow[f], a.lgb_zero_map) : nan_value<XT>();
+        }
+        const int32_t next = go_left<ZERO>(x, thr[q], nd[q].y) ? (int32_t)nd[q].z : (int32_t)nd[q].w;
+        c[q] = c[q] < 0 ? c[q] : next;
+        active |= c[q] >= 0;
+      }
+      if (__ballot(active) == 0) break;
+    }
+#pragma unroll
+    for (int q = 0; q < kExpIlp; ++q) {
+      const int t = t0 + q;
+      if (t < T) {
+        const int64_t lb = a.leaf_base[t];
+        if (want_leaf) {
+          if (live) out_leaf[row * T + t] = a.exp_leaf_ids[lb + (~c[q])];
+        } else {
+          add_leaf<ACC, KMAX>(acc, leaves + lb * a.leaf_width, ~c[q], a.leaf_width,
+                              a.tree_group[t]);
+        }
+      }
     }
   }
   if (!live || want_leaf) return;

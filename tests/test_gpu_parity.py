@@ -271,3 +271,94 @@ def test_leafwise_lgb_full_property():
     got = dev.predict(X, OUT_MARGIN)
     want = port.lgb_predict_raw(trees, 1, 100, X.astype(np.float64))[:, 0]
     assert np.array_equal(got, want)
+
+
+# ------------------------------------------------- every layout, same forest
+def _dev_with_layout(forest, layout):
+    old = os.environ.get("TI_FORCE_LAYOUT")
+    os.environ["TI_FORCE_LAYOUT"] = layout
+    try:
+        return DeviceForest(forest, [0])
+    finally:
+        if old is None:
+            del os.environ["TI_FORCE_LAYOUT"]
+        else:
+            os.environ["TI_FORCE_LAYOUT"] = old
+
+
+LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2}
+
+
+@pytest.mark.parametrize("layout", ["heap", "compact", "explicit"])
+def test_xgb_golden_every_layout(golden, layout):
+    g = np.load(os.path.join(golden, "xgb_synth.npz"))
+    trees, ti = xf.synthetic_complete_trees(40, 8, 28, seed=1)
+    dev = _dev_with_layout(xf.forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic"),
+                           layout)
+    assert dev.info()["layout"] == LAYOUT_ID[layout]
+    assert np.array_equal(dev.predict(g["X"], OUT_MARGIN), g["margin"])
+    assert np.array_equal(dev.predict(g["X"], OUT_LEAF), g["leaf"])
+    trees3, ti3 = xf.synthetic_complete_trees(30, 6, 28, seed=2, num_class=3)
+    dev3 = _dev_with_layout(xf.forest_from_raw_trees(trees3, ti3, 28, 3, 0.5, "multi:softprob"),
+                            layout)
+    assert np.array_equal(dev3.predict(g["X"], OUT_MARGIN), g["margin3"])
+    np.testing.assert_allclose(dev3.predict(g["X"], OUT_PREDICT), g["prob3"], rtol=RTOL)
+
+
+@pytest.mark.parametrize("layout", ["compact", "explicit"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
+    g = np.load(os.path.join(golden, "lgb_synth.npz"))
+    trees = lf.synthetic_leafwise_trees(20, 63, 28, seed=3)
+    p = str(tmp_path / "model.txt")
+    lf.write_lightgbm_text(p, trees, 28, "binary sigmoid:1")
+    f = load_lightgbm_model(p)
+    dev = _dev_with_layout(f, layout)
+    assert dev.info()["layout"] == LAYOUT_ID[layout]
+    lm = lgb_ref.read_lgb_text(p)
+    X = g["X"].astype(dtype)
+    Xd = X.astype(np.float64)
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), lgb_ref.predict(lm, Xd, raw_score=True))
+    assert np.array_equal(dev.predict(X, OUT_LEAF), lgb_ref.leaf_index(lm, Xd))
+
+
+@pytest.mark.parametrize("layout", ["heap", "compact", "explicit"])
+def test_lgb_iris_fixture_every_layout(golden, layout):
+    from sklearn.datasets import load_iris
+    path = os.path.join(golden, "lgb_iris_v3.txt")
+    dev = _dev_with_layout(load_lightgbm_model(path), layout)
+    m = lgb_ref.read_lgb_text(path)
+    X = load_iris()["data"]
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), lgb_ref.predict(m, X, raw_score=True))
+
+
+@pytest.mark.parametrize("layout", ["compact", "explicit"])
+def test_sklearn_classifier_every_layout(golden, layout):
+    fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
+    gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
+    dev = _dev_with_layout(fc, layout)
+    if dev.info()["layout"] != LAYOUT_ID[layout]:
+        pytest.skip("trees too large for the compact layout")
+    assert np.array_equal(dev.predict(gc["X"], OUT_MARGIN), gc["predict_proba"])
+    assert np.array_equal(dev.predict(gc["X"], OUT_LEAF), gc["apply"])
+
+
+@pytest.mark.parametrize("rows", [1, 127, 129, 1000])
+def test_compact_ragged_and_specials(rows):
+    trees = lf.synthetic_leafwise_trees(37, 255, 40, seed=5)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, 40, "binary sigmoid:1")
+        f = load_lightgbm_model(p)
+    dev = DeviceForest(f, [0])
+    assert dev.info()["layout"] == 2
+    rng = np.random.default_rng(rows)
+    X = rng.standard_normal((rows, 40))
+    sp = np.array([np.nan, 0.0, -0.0, 1e-40, np.inf, -np.inf])
+    mask = rng.random(X.shape) < 0.1
+    X[mask] = sp[rng.integers(0, len(sp), mask.sum())]
+    want = port.lgb_predict_raw(trees, 1, 40, X)[:, 0]
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), want)
+    X32 = X.astype(np.float32)
+    assert np.array_equal(dev.predict(X32, OUT_MARGIN),
+                          port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
