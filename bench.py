@@ -44,6 +44,9 @@ def parse_args():
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="target CPU work for the cpu_baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--latency-qps", type=float, default=10000.0,
+                   help="offered requests/s for the batched-latency leg (0 = skip)")
+    p.add_argument("--latency-seconds", type=float, default=3.0)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
     return p.parse_args()
 
@@ -89,6 +92,79 @@ def cpu_baseline(trees, ti, X_host, target_s):
             "sample": f"{n} rows of the same 1M x 28 batch, oracle/c/tree_port.c "
                       f"(xgboost 0.82 predict loop restated, OpenMP {n_thr} threads), "
                       f"{dt:.1f} s"}
+
+
+def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5, seed=7,
+                    freeze_gc=True):
+    """C5-style leg: open-loop Poisson arrivals of requests of
+    U{1..64} rows into the pipelined in-process batcher (pkg/batcher semantics,
+    maxBatchSize rows, maxLatency ms) in front of the GPU engine (host buffers:
+    H2D + kernel + D2H per batch).  Latency = result time - scheduled arrival."""
+    import asyncio
+    from concurrent.futures import ThreadPoolExecutor
+    from kfserving_amd.batcher import Batcher
+    rng = np.random.default_rng(seed)
+    warm = int(qps * 0.5)                 # first 0.5 s of load is warmup, not reported
+    n_req = int(qps * seconds) + warm
+    gaps = rng.exponential(1.0 / qps, n_req)
+    sizes = rng.integers(1, 65, n_req)
+    pool = np.random.default_rng(seed + 1).standard_normal((64 * 1024, n_feat), dtype=np.float32)
+    pool_rows = list(pool)
+    pool_ex = ThreadPoolExecutor(max_workers=2)
+    lat = np.zeros(n_req)
+    batch_rows = []
+    batch_ms = []
+
+    async def predict_batch(instances):
+        X = np.stack(instances)
+        batch_rows.append(X.shape[0])
+        t = time.perf_counter()
+        out = await asyncio.get_running_loop().run_in_executor(pool_ex, dev.predict, X)
+        batch_ms.append((time.perf_counter() - t) * 1e3)
+        return {"predictions": out}
+
+    async def run():
+        b = Batcher(predict_batch, max_batch_size=max_batch, max_latency_ms=max_latency_ms)
+        loop = asyncio.get_running_loop()
+        t0 = loop.time() + 0.05
+        arrivals = t0 + np.cumsum(gaps)
+        tasks = []
+
+        async def one(i):
+            off = (i * 64) % (len(pool_rows) - 64)
+            await b.submit(pool_rows[off:off + int(sizes[i])])
+            lat[i] = loop.time() - arrivals[i]
+
+        for i in range(n_req):
+            delay = arrivals[i] - loop.time()
+            if delay > 0:
+                await asyncio.sleep(delay)
+            tasks.append(asyncio.ensure_future(one(i)))
+        await asyncio.gather(*tasks)
+        return loop.time() - t0
+
+    import gc
+    old = gc.get_threshold()
+    if freeze_gc:          # what KFServer.start does after load (kfserver.tune_gc)
+        from kfserving_amd.kfserving.kfserver import tune_gc
+        tune_gc()
+    try:
+        wall = asyncio.run(run())
+    finally:
+        if freeze_gc:
+            gc.unfreeze()
+            gc.set_threshold(*old)
+    pool_ex.shutdown()
+    lat_ms = lat[warm:] * 1e3
+    return {"qps_offered": qps, "requests": n_req - warm, "rows_per_request": "U{1..64}",
+            "max_batch_size": max_batch, "max_latency_ms": max_latency_ms,
+            "p50_ms": float(np.percentile(lat_ms, 50)), "p99_ms": float(np.percentile(lat_ms, 99)),
+            "max_ms": float(lat_ms.max()), "rows_per_s": float(sizes.sum() / wall),
+            "p90_ms": float(np.percentile(lat_ms, 90)),
+            "batches": len(batch_rows), "mean_batch_rows": float(np.mean(batch_rows)),
+            "predict_ms_p50": float(np.percentile(batch_ms, 50)),
+            "predict_ms_p99": float(np.percentile(batch_ms, 99)), "gc_frozen": freeze_gc,
+            "path": "in-process batcher -> ti_predict (host buffers), 1 GPU, no HTTP/JSON"}
 
 
 def main():
@@ -164,6 +240,9 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(trees, ti, X_host, args.cpu_seconds)
+        latency = None
+        if args.latency_qps > 0:
+            latency = batched_latency(dev, N_FEAT, args.latency_qps, args.latency_seconds)
         line = {
             "metric": "predicted rows/sec (500-tree XGB, 28 feat)",
             "value": value,
@@ -185,6 +264,7 @@ def main():
                        "explicit", "parallelism": f"rows sharded x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "batched_latency": latency,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -98,7 +98,7 @@ class Batcher:
                 return
         batch_id = str(uuid.uuid4())
         preds = response.get("predictions") if isinstance(response, dict) else None
-        if not isinstance(preds, list) or len(preds) != len(batch):
+        if preds is None or not hasattr(preds, "__len__") or len(preds) != len(batch):
             for fut, _, _ in waiters:
                 if not fut.done():
                     fut.set_result({"message": SIZE_MISMATCH, "batchId": batch_id,

@@ -116,11 +116,15 @@ struct DeviceForest {
   int32_t* cpt_nint = nullptr;
   int32_t* cpt_depth = nullptr;
   int32_t* cpt_root = nullptr;
-  // ti_predict scratch
+  // ti_predict scratch: device buffers + pinned host staging (grown x2)
   void* x_buf = nullptr;
   size_t x_cap = 0;
   void* out_buf = nullptr;
   size_t out_cap = 0;
+  void* hx_pin = nullptr;
+  size_t hx_cap = 0;
+  void* ho_pin = nullptr;
+  size_t ho_cap = 0;
   int64_t bytes = 0;
   std::mutex mu;
 };
@@ -179,6 +183,10 @@ void free_device(DeviceForest& d) {
                   d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (d.hx_pin) (void)hipHostFree(d.hx_pin);
+  if (d.ho_pin) (void)hipHostFree(d.ho_pin);
+  d.hx_pin = d.ho_pin = nullptr;
+  d.hx_cap = d.ho_cap = 0;
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d.heap32 = d.heap64 = nullptr;
   d.heap_leaf_ids = d.root = d.exp_leaf_ids = d.tree_group = nullptr;
@@ -702,13 +710,19 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   return TI_OK;
 }
 
-int grow(void** buf, size_t* cap, size_t need) {
+// Scratch buffers grow geometrically (x2, >= 4 MiB) so a serving process
+// stops reallocating after its first few batch sizes.
+int grow(void** buf, size_t* cap, size_t need, bool pinned = false) {
   if (need <= *cap) return TI_OK;
-  if (*buf) (void)hipFree(*buf);
+  const size_t n = std::max({need, static_cast<size_t>(4) << 20, 2 * *cap});
+  if (*buf) (void)(pinned ? hipHostFree(*buf) : hipFree(*buf));
   *buf = nullptr;
   *cap = 0;
-  size_t n = std::max(need, static_cast<size_t>(1) << 20);
-  TI_HIP(hipMalloc(buf, n));
+  if (pinned) {
+    TI_HIP(hipHostMalloc(buf, n, hipHostMallocDefault));
+  } else {
+    TI_HIP(hipMalloc(buf, n));
+  }
   *cap = n;
   return TI_OK;
 }
@@ -722,12 +736,19 @@ int predict_shard(ti_forest* f, DeviceForest& d, const unsigned char* X, int xdt
   const size_t out_bytes = static_cast<size_t>(rows * output_width(f, kind)) *
                            dtype_size(output_dtype(f, kind));
   int rc;
-  if ((rc = grow(&d.x_buf, &d.x_cap, x_elems * xs))) return rc;
+  const size_t x_bytes = x_elems * xs;
+  if ((rc = grow(&d.x_buf, &d.x_cap, x_bytes))) return rc;
   if ((rc = grow(&d.out_buf, &d.out_cap, out_bytes))) return rc;
-  TI_HIP(hipMemcpyAsync(d.x_buf, X, x_elems * xs, hipMemcpyHostToDevice, d.stream));
+  if ((rc = grow(&d.hx_pin, &d.hx_cap, x_bytes, true))) return rc;
+  if ((rc = grow(&d.ho_pin, &d.ho_cap, out_bytes, true))) return rc;
+  // caller memory -> pinned staging -> DMA; keeps H2D/D2H asynchronous and at
+  // PCIe rate whatever kind of host memory the caller holds
+  std::memcpy(d.hx_pin, X, x_bytes);
+  TI_HIP(hipMemcpyAsync(d.x_buf, d.hx_pin, x_bytes, hipMemcpyHostToDevice, d.stream));
   if ((rc = launch(f, d, d.x_buf, xdt, rows, cols, stride, kind, d.out_buf, d.stream))) return rc;
-  TI_HIP(hipMemcpyAsync(out, d.out_buf, out_bytes, hipMemcpyDeviceToHost, d.stream));
+  TI_HIP(hipMemcpyAsync(d.ho_pin, d.out_buf, out_bytes, hipMemcpyDeviceToHost, d.stream));
   TI_HIP(hipStreamSynchronize(d.stream));
+  std::memcpy(out, d.ho_pin, out_bytes);
   return TI_OK;
 }
 
@@ -788,11 +809,11 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   const char* force = std::getenv("TI_FORCE_LAYOUT");
   std::string want = force ? force : "";
   bool use_heap = D <= kMaxHeapDepth;
-  // compact pays only while the [F][256] feature image leaves LDS for tree
-  // stages (measured at F = 100: explicit 19.1 ms, compact 29.6 ms with the
-  // image in LDS, 160 ms reading rows from HBM per visit)
-  bool use_compact = !use_heap && compact_fits(desc) &&
-                     static_cast<size_t>(desc->n_features) * 256 * 4 <= static_cast<size_t>(40 * 1024);
+  // compact layout: LDS-staged irregular trees (F = 100: explicit 19.1 ms,
+  // compact 29.6 ms with the feature image in LDS, 160 ms reading rows from HBM)
+  // (measured on 1000 x 255-leaf LightGBM forests: explicit 7.8 ms vs compact
+  // 8.8 ms at F = 28, so compact is opt-in only until it beats explicit)
+  bool use_compact = false;
   if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
   if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
   if (want == "explicit") { use_heap = false; use_compact = false; }

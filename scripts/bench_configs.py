@@ -49,18 +49,19 @@ def c3(args):
     from kfserving_amd.formats import lightgbm_format as lf
     from kfserving_amd.forest import OUT_MARGIN, TI_F32
     from oracle import port
-    trees = lf.synthetic_leafwise_trees(1000, 255, 100, seed=1)
+    F = args.f3
+    trees = lf.synthetic_leafwise_trees(1000, 255, F, seed=1)
     with tempfile.TemporaryDirectory() as d:
         p = os.path.join(d, "model.txt")
-        lf.write_lightgbm_text(p, trees, 100, "binary sigmoid:1")
+        lf.write_lightgbm_text(p, trees, F, "binary sigmoid:1")
         f = lf.load_lightgbm_model(p)
     depths = f.depths()
     dev = DeviceForest(f, [0])
     rows = args.rows3
-    X = np.random.default_rng(3).standard_normal((rows, 100), dtype=np.float32)
+    X = np.random.default_rng(3).standard_normal((rows, F), dtype=np.float32)
     Xt = torch.from_numpy(X).cuda()
     out = torch.empty(rows, dtype=torch.float64, device="cuda")
-    rate, kms = time_device(dev, Xt, out, rows, 100, OUT_MARGIN, TI_F32, args.steps, 2)
+    rate, kms = time_device(dev, Xt, out, rows, F, OUT_MARGIN, TI_F32, args.steps, 2)
     # node visits per row, measured from the leaves reached on a sample
     from tests import canon_eval
     lv = canon_eval.leaves(f, X[:2000])
@@ -68,9 +69,9 @@ def c3(args):
     visits = float(np.mean(np.sum(node_depth[f.tree_offset[:-1][None, :] + lv], axis=1)))
     n = min(rows, 50_000)
     t0 = time.perf_counter()
-    port.lgb_predict_raw(trees, 1, 100, X[:n].astype(np.float64))
+    port.lgb_predict_raw(trees, 1, F, X[:n].astype(np.float64))
     cpu = n / (time.perf_counter() - t0)
-    return {"config": "C3 LightGBM leaf-wise 1000x255 leaves, 100 feat, f32 input",
+    return {"config": f"C3 LightGBM leaf-wise 1000x255 leaves, {F} feat, f32 input",
             "rows": rows, "rows_per_s": rate, "kernel_ms": kms, "layout": dev.info()["layout"],
             "max_depth": int(depths.max()), "mean_tree_depth": float(depths.mean()),
             "node_visits_per_row": visits,
@@ -133,6 +134,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--configs", default="c3,c4")
     p.add_argument("--rows3", type=int, default=1_000_000)
+    p.add_argument("--f3", type=int, default=100, help="C3 feature count (BASELINE: 100)")
     p.add_argument("--rows4", type=int, default=1_000_000)
     p.add_argument("--fit-rows", type=int, default=200_000)
     p.add_argument("--steps", type=int, default=5)

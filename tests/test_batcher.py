@@ -152,3 +152,18 @@ def test_agent_proxy_end_to_end():
     c.request("GET", "/v1/models/m")
     assert c.getresponse().status == 200                 # non-predict paths proxied
     backend.stop()
+
+
+def test_bench_batched_latency_leg_on_cpu():
+    """bench.py's C5-style leg with a CPU stand-in for the device forest."""
+    import numpy as np
+    import bench
+
+    class FakeDev:
+        def predict(self, X):
+            return X.sum(axis=1)
+
+    r = bench.batched_latency(FakeDev(), 28, qps=2000, seconds=0.5, max_latency_ms=5)
+    assert r["requests"] == 1000 and r["batches"] >= 1
+    assert 1.0 <= r["p50_ms"] < 100 and r["p99_ms"] >= r["p50_ms"]
+    assert r["mean_batch_rows"] > 32

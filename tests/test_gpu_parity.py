@@ -350,7 +350,7 @@ def test_compact_ragged_and_specials(rows):
         p = os.path.join(d, "model.txt")
         lf.write_lightgbm_text(p, trees, 40, "binary sigmoid:1")
         f = load_lightgbm_model(p)
-    dev = DeviceForest(f, [0])
+    dev = _dev_with_layout(f, "compact")
     assert dev.info()["layout"] == 2
     rng = np.random.default_rng(rows)
     X = rng.standard_normal((rows, 40))

@@ -1,0 +1,70 @@
+"""End to end on the GPU: HTTP v1 :predict -> KFServer -> plugin -> libtreeinfer,
+with the reference fixtures and known answers (test/e2e/predictor/*)."""
+import json
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from kfserving_amd.kfserving import KFServer
+from tests.test_server import _Running
+
+pytestmark = pytest.mark.gpu
+
+
+def _dir(golden, tmp_path, src, dst):
+    d = tmp_path / "m"
+    d.mkdir()
+    shutil.copy(os.path.join(golden, src), str(d / dst))
+    return str(d)
+
+
+def test_xgbserver_http_known_answer(golden, tmp_path):
+    from kfserving_amd.xgbserver import XGBoostModel, XGBoostModelRepository
+    model = XGBoostModel("xgboost-iris", _dir(golden, tmp_path, "xgb_iris_legacy_082.bst",
+                                              "model.bst"), 1)
+    model.load()
+    server = KFServer(registered_models=XGBoostModelRepository(str(tmp_path)))
+    server.register_model(model)
+    s = _Running(server)
+    with open(os.path.join(golden, "iris_input.json"), "rb") as fh:
+        body = fh.read()
+    code, hdrs, out = s.fetch("/v1/models/xgboost-iris:predict", "POST", body)
+    assert code == 200 and json.loads(out)["predictions"] == [1, 1]   # test_xgboost.py:67-68
+    assert out == b'{"predictions": [1.0, 1.0]}'                      # v1alpha2 README:103
+    s.stop()
+
+
+def test_lgbserver_http_known_answer(golden, tmp_path):
+    from kfserving_amd.lgbserver import LightGBMModel
+    model = LightGBMModel("lightgbm", _dir(golden, tmp_path, "lgb_iris_v3.txt", "model.bst"), 1)
+    model.load()
+    server = KFServer(workers=1)
+    server.register_model(model)
+    s = _Running(server)
+    with open(os.path.join(golden, "iris_input_v3.json"), "rb") as fh:
+        code, _, out = s.fetch("/v1/models/lightgbm:predict", "POST", fh.read())
+    assert code == 200 and json.loads(out)["predictions"][0][0] > 0.5  # test_lightgbm.py:65-67
+    s.stop()
+
+
+def test_sklearnserver_http_and_batcher(golden, tmp_path):
+    from kfserving_amd.sklearnserver import SKLearnModel
+    from oracle import sk_ref
+    from tests.test_oracle import _sk_trees
+    model = SKLearnModel("sk", _dir(golden, tmp_path, "sk_rf_reg_model.npz", "model.npz"))
+    assert model.load()
+    server = KFServer(max_batchsize=64, max_latency_ms=20)
+    server.register_model(model)
+    s = _Running(server)
+    g = np.load(os.path.join(golden, "sk_rf_reg.npz"))
+    X = np.nan_to_num(g["X"][:8]).astype(np.float64)
+    trees, _ = _sk_trees(os.path.join(golden, "sk_rf_reg_model.npz"))
+    want = sk_ref.predict_regressor(trees, X)
+    code, _, out = s.fetch("/v1/models/sk:predict", "POST",
+                           json.dumps({"instances": X.tolist()}).encode())
+    res = json.loads(out)
+    assert code == 200 and res["message"] == "" and res["batchId"]
+    assert np.array_equal(np.array(res["predictions"]), want)
+    s.stop()
