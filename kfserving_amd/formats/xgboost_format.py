@@ -8,7 +8,8 @@ python/xgbserver/xgbserver/model.py:38-39 without importing xgboost.  Reads:
   example_model/model/model.bst),
 * the 1.x binary with the ``binf`` magic (fixture docs/samples/v1beta1/
   xgboost/model.bst), and
-* the JSON model (xgboost >= 1.0 ``save_model("*.json")``).
+* the JSON model (xgboost >= 1.0 ``save_model("*.json")``) and its UBJSON
+  form (xgboost >= 1.6 default ``.ubj``).
 
 Predict semantics encoded (upstream xgboost 0.82 ``RegTree::GetNext`` /
 ``CPUPredictor::PredValue``): go left iff ``x < split`` in float32, a missing
@@ -255,11 +256,22 @@ def parse_xgboost_bytes(buf: bytes) -> Forest:
         return _parse_binary(base64.b64decode(buf[4:]), 0, "legacy-b64")
     head = buf.lstrip()[:1]
     if head == b"{":
+        # JSON text continues with whitespace or a quoted key; UBJSON with a
+        # length marker ('U', 'i', 'l', ...) or a container header ('$', '#')
+        if buf[1:2] in (b'"', b" ", b"\n", b"\r", b"\t", b"}"):
+            try:
+                doc = json.loads(buf.decode("utf-8"))
+            except (UnicodeDecodeError, json.JSONDecodeError) as e:
+                raise XGBoostFormatError(f"malformed JSON model: {e}") from e
+            return _parse_json(doc)
+        from . import ubjson
         try:
-            doc = json.loads(buf.decode("utf-8"))
-        except (UnicodeDecodeError, json.JSONDecodeError) as e:
-            raise XGBoostFormatError(f"UBJSON models are not supported yet ({e})") from e
-        return _parse_json(doc)
+            doc = ubjson.loads(buf)
+        except (ubjson.UBJSONError, KeyError, UnicodeDecodeError) as e:
+            raise XGBoostFormatError(f"malformed UBJSON model: {e}") from e
+        f = _parse_json(doc)
+        f.meta["format"] = "ubj"
+        return f
     return _parse_binary(buf, 0, "legacy")
 
 
@@ -312,23 +324,26 @@ def write_legacy_binary(path: str, trees: List[dict], tree_info, num_feature: in
         fh.write(bytes(out))
 
 
-def write_json_model(path: str, trees: List[dict], tree_info, num_feature: int, num_class: int,
-                     base_score: float, objective: str, version=(1, 3, 0)) -> None:
-    """Write the same model as xgboost >= 1.0 JSON (subset the loader reads)."""
+def json_model_doc(trees: List[dict], tree_info, num_feature: int, num_class: int,
+                   base_score: float, objective: str, version=(1, 3, 0), arrays=False) -> dict:
+    """The xgboost >= 1.0 JSON model document (subset the loader reads);
+    ``arrays=True`` keeps numpy arrays (for the UBJSON writer)."""
     jt = []
     for i, t in enumerate(trees):
         n = len(t["cleft"])
+        conv = (lambda a, dt: np.asarray(a, dtype=dt)) if arrays else \
+            (lambda a, dt: [dt(v).item() for v in np.asarray(a, dtype=dt)])
         jt.append({
             "id": i,
-            "left_children": [int(v) for v in t["cleft"]],
-            "right_children": [int(v) for v in t["cright"]],
-            "split_indices": [int(v) & 0x7FFFFFFF for v in t["sindex"]],
-            "default_left": [int(v) >> 31 for v in t["sindex"]],
-            "split_conditions": [float(np.float32(v)) for v in t["value"]],
+            "left_children": conv(t["cleft"], np.int32),
+            "right_children": conv(t["cright"], np.int32),
+            "split_indices": conv(np.asarray(t["sindex"]) & 0x7FFFFFFF, np.int32),
+            "default_left": conv(np.asarray(t["sindex"]) >> 31, np.uint8),
+            "split_conditions": conv(t["value"], np.float32),
             "tree_param": {"num_nodes": str(n), "num_feature": str(num_feature),
                            "size_leaf_vector": "0"},
         })
-    doc = {
+    return {
         "version": list(version),
         "learner": {
             "attributes": {},
@@ -339,10 +354,27 @@ def write_json_model(path: str, trees: List[dict], tree_info, num_feature: int, 
             "objective": {"name": objective},
             "gradient_booster": {"name": "gbtree", "model": {
                 "gbtree_model_param": {"num_trees": str(len(trees)), "size_leaf_vector": "0"},
-                "tree_info": [int(v) for v in tree_info],
+                "tree_info": np.asarray(tree_info, dtype=np.int32) if arrays
+                else [int(v) for v in tree_info],
                 "trees": jt}},
         },
     }
+
+
+def write_ubj_model(path: str, trees: List[dict], tree_info, num_feature: int, num_class: int,
+                    base_score: float, objective: str, version=(1, 6, 0)) -> None:
+    """Write the model as xgboost >= 1.6 UBJSON."""
+    from . import ubjson
+    doc = json_model_doc(trees, tree_info, num_feature, num_class, base_score, objective,
+                         version, arrays=True)
+    with open(path, "wb") as fh:
+        fh.write(ubjson.dumps(doc))
+
+
+def write_json_model(path: str, trees: List[dict], tree_info, num_feature: int, num_class: int,
+                     base_score: float, objective: str, version=(1, 3, 0)) -> None:
+    """Write the same model as xgboost >= 1.0 JSON (subset the loader reads)."""
+    doc = json_model_doc(trees, tree_info, num_feature, num_class, base_score, objective, version)
     with open(path, "w") as fh:
         json.dump(doc, fh)
 

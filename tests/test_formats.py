@@ -69,9 +69,14 @@ def test_xgb_writers_roundtrip(tmp_path):
     trees, ti = xf.synthetic_complete_trees(12, 5, 10, seed=4, num_class=3)
     pb = str(tmp_path / "m.bst")
     pj = str(tmp_path / "m.json")
+    pu = str(tmp_path / "m.ubj")
     xf.write_legacy_binary(pb, trees, ti, 10, 3, 0.5, "multi:softprob")
     xf.write_json_model(pj, trees, ti, 10, 3, 0.5, "multi:softprob")
-    fb, fj = load_xgboost_model(pb), load_xgboost_model(pj)
+    xf.write_ubj_model(pu, trees, ti, 10, 3, 0.5, "multi:softprob")
+    fb, fj, fu = load_xgboost_model(pb), load_xgboost_model(pj), load_xgboost_model(pu)
+    assert fu.meta["format"] == "ubj" and fj.meta["format"] == "json"
+    for k in ("feature", "threshold", "flags", "left", "right", "leaf_value", "tree_group"):
+        assert np.array_equal(getattr(fu, k), getattr(fj, k)), k
     m = xgb_ref.read_xgb_binary(pb)
     rng = np.random.default_rng(0)
     X = rng.standard_normal((300, 10)).astype(np.float32)
@@ -79,6 +84,22 @@ def test_xgb_writers_roundtrip(tmp_path):
     want = xgb_ref.predict(m, X, output_margin=True)
     np.testing.assert_array_equal(canon_eval.predict(fb, X, OUT_MARGIN), want)
     np.testing.assert_array_equal(canon_eval.predict(fj, X, OUT_MARGIN), want)  # base 0.5 identity
+    # .ubj carries version 1.6: xgboost >= 1.4 starts the sum at base_score
+    # (base first), so margins match within float32 rounding, not bitwise
+    assert fu.base_first and not fb.base_first
+    np.testing.assert_allclose(canon_eval.predict(fu, X, OUT_MARGIN), want, rtol=1e-6)
+
+
+def test_ubjson_roundtrip_values():
+    from kfserving_amd.formats import ubjson
+    doc = {"a": [1, 2.5, "x", True, None, {"b": []}], "f": np.arange(300, dtype=np.float32),
+           "i": np.arange(5, dtype=np.int32), "s": "é" * 300}
+    back = ubjson.loads(ubjson.dumps(doc))
+    assert back["a"] == [1, 2.5, "x", True, None, {"b": []}] and back["s"] == doc["s"]
+    assert np.array_equal(back["f"], doc["f"]) and back["f"].dtype == np.float32
+    assert np.array_equal(back["i"], doc["i"])
+    with pytest.raises(ubjson.UBJSONError):
+        ubjson.loads(b"[$d#U\x05\x00")
 
 
 def test_xgb_threshold_encoding_edges():
