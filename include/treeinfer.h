@@ -41,6 +41,12 @@
  *     else if x == 0 and (flags[n] & TI_NODE_ZERO_FLIP):
  *                             go left iff !(0 <= threshold[n])
  *     else:                   go left iff x <= threshold[n]
+ *   categorical nodes (flags[n] & TI_NODE_CATEGORICAL; LightGBM
+ *   Tree::CategoricalDecision, decision_type bit 0) replace all of the above:
+ *     v = (int)x truncated toward zero; NaN, x <= -1 and x >= 2^31 go right
+ *     (static_cast<int> yields INT_MIN there on x86, which LightGBM sends right);
+ *     go left iff v / 32 < cat_nwords[n] and bit v % 32 of
+ *     cat_bits[cat_offset[n] + v / 32] is set (Common::FindInBitset).
  *   The host encodes each library's rule into threshold/flags:
  *     XGBoost  (x < t, f32)  : threshold = nextafterf(t, -inf) (NaN if t=-inf),
  *                              NAN_LEFT = default_left
@@ -59,7 +65,7 @@
 extern "C" {
 #endif
 
-#define TI_ABI_VERSION 1
+#define TI_ABI_VERSION 2
 
 /* return codes */
 #define TI_OK               0
@@ -76,6 +82,7 @@ extern "C" {
 /* node flag bits (ti_forest_desc.flags) */
 #define TI_NODE_NAN_LEFT   0x01  /* NaN input goes left                    */
 #define TI_NODE_ZERO_FLIP  0x02  /* x == 0 takes the opposite of (0 <= t)  */
+#define TI_NODE_CATEGORICAL 0x04 /* bitset membership split (LightGBM)     */
 
 /* output transforms applied after accumulation (ti_forest_desc.transform) */
 #define TI_TRANSFORM_IDENTITY    0
@@ -123,6 +130,12 @@ typedef struct ti_forest_desc {
   int32_t transform;          /* TI_TRANSFORM_*                                     */
   int32_t reserved0;
   double  transform_param;    /* sigmoid scale                                      */
+  /* categorical splits (ABI 2); NULL / 0 when the forest has none.  Replaces
+   * cat_boundaries / cat_threshold of a LightGBM tree (tree.h, model text v3). */
+  int64_t n_cat_words;        /* W                                                  */
+  const uint32_t* cat_bits;   /* [W]   bitset words of all categorical nodes        */
+  const int64_t* cat_offset;  /* [N]   first word of node n's bitset                */
+  const int32_t* cat_nwords;  /* [N]   words in node n's bitset                     */
 } ti_forest_desc;
 
 typedef struct ti_forest ti_forest;   /* opaque, owns device memory */

@@ -108,6 +108,7 @@ struct DeviceForest {
   int64_t* leaf_base = nullptr;
   void* leaves = nullptr;
   int32_t* exp_leaf_ids = nullptr;
+  uint32_t* cat_words = nullptr;
   int32_t* tree_group = nullptr;
   // compact layout
   unsigned char* cpt_img[2] = {nullptr, nullptr};
@@ -157,6 +158,8 @@ struct ti_forest {
   std::vector<double> h_thr64;
   std::vector<int64_t> h_node_base, h_leaf_base;
   std::vector<int32_t> h_root, h_exp_leaf_ids, h_group;
+  std::vector<uint32_t> h_cat_words;   // [nwords, w0, w1, ...] per categorical node
+  int32_t has_cat = 0;
   std::vector<unsigned char> h_leaves;   // ACC-typed
   std::vector<std::unique_ptr<DeviceForest>> devs;
 };
@@ -180,7 +183,7 @@ void free_device(DeviceForest& d) {
   void* ptrs[] = {d.heap32, d.heap64, d.heap_leaf_ids, d.nodes, d.thr64, d.node_base, d.root,
                   d.leaf_base, d.leaves, d.exp_leaf_ids, d.tree_group, d.x_buf, d.out_buf,
                   d.cpt_img[0], d.cpt_img[1], d.cpt_off[0], d.cpt_off[1], d.cpt_stage[0],
-                  d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root};
+                  d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root, d.cat_words};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d.hx_pin) (void)hipHostFree(d.hx_pin);
@@ -200,6 +203,7 @@ void free_device(DeviceForest& d) {
     d.cpt_stage[i] = nullptr;
   }
   d.cpt_nint = d.cpt_depth = d.cpt_root = nullptr;
+  d.cat_words = nullptr;
   d.x_cap = d.out_cap = 0;
   d.stream = nullptr;
   d.device = -1;
@@ -254,6 +258,13 @@ int validate(const ti_forest_desc* d, std::vector<int>* depth_out) {
       }
       if (d->feature[g] >= d->n_features)
         return fail(TI_ERR_INVALID, "split feature >= n_features in tree " + std::to_string(t));
+      if (d->flags[g] & TI_NODE_CATEGORICAL) {
+        if (!d->cat_bits || !d->cat_offset || !d->cat_nwords)
+          return fail(TI_ERR_INVALID, "categorical node without cat_bits/cat_offset/cat_nwords");
+        const int64_t o = d->cat_offset[g], w = d->cat_nwords[g];
+        if (o < 0 || w < 0 || o + w > d->n_cat_words)
+          return fail(TI_ERR_INVALID, "categorical bitset out of range in tree " + std::to_string(t));
+      }
       const int32_t l = d->left[g], r = d->right[g];
       if (l < 0 || l >= n || r < 0 || r >= n)
         return fail(TI_ERR_INVALID, "child index out of range in tree " + std::to_string(t));
@@ -326,6 +337,7 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
   f->h_leaf_base.assign(d->n_trees, 0);
   f->h_root.assign(d->n_trees, 0);
   f->h_exp_leaf_ids.clear();
+  f->h_cat_words.clear();
   std::vector<ACC> leaves;
   std::vector<int32_t> remap;
   std::vector<int32_t> queue;
@@ -363,6 +375,15 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
       ExpNode e;
       e.thr = round_down_f32(d->threshold[g]);
       e.meta = make_meta(d->feature[g], d->flags[g]);
+      if (d->flags[g] & TI_NODE_CATEGORICAL) {
+        // threshold slot carries the word offset of [nwords, bitset...]
+        const uint32_t at = static_cast<uint32_t>(f->h_cat_words.size());
+        const int32_t nw = d->cat_nwords[g];
+        f->h_cat_words.push_back(static_cast<uint32_t>(nw));
+        for (int32_t w = 0; w < nw; ++w) f->h_cat_words.push_back(d->cat_bits[d->cat_offset[g] + w]);
+        std::memcpy(&e.thr, &at, sizeof(at));
+        e.meta = (static_cast<uint32_t>(d->feature[g]) & ti::kMetaFeatMask) | ti::kMetaCat;
+      }
       e.left = remap[d->left[g]];
       e.right = remap[d->right[g]];
       f->h_nodes[nb + remap[v]] = e;
@@ -522,6 +543,7 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
     if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
     d.leaves = lv;
     if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
+    if ((rc = upload(&d.cat_words, f->h_cat_words, &d.bytes))) return rc;
   }
   return TI_OK;
 }
@@ -699,6 +721,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.leaf_base = d.leaf_base;
     a.leaves = d.leaves;
     a.exp_leaf_ids = d.exp_leaf_ids;
+    a.cat_words = d.cat_words;
   }
   KernelFn fn = select_kernel(f->layout, xdt, f->accum, f->K, feat_lds, f->zero_rule != 0);
   int rc = ensure_lds_attr(d.device, fn);
@@ -795,7 +818,10 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   f->divisor = desc->average_divisor;
   for (int k = 0; k < f->K; ++k) f->base[k] = desc->base_margin[k];
   for (int64_t i = 0; i < desc->n_nodes; ++i)
-    if (desc->feature[i] >= 0 && (desc->flags[i] & TI_NODE_ZERO_FLIP)) f->zero_rule = 1;
+    if (desc->feature[i] >= 0) {
+      if (desc->flags[i] & TI_NODE_CATEGORICAL) f->has_cat = 1;
+      else if (desc->flags[i] & TI_NODE_ZERO_FLIP) f->zero_rule = 1;
+    }
   f->h_group.assign(f->T, 0);
   if (f->LW == 1)
     for (int t = 0; t < f->T; ++t) f->h_group[t] = desc->tree_group[t];
@@ -817,6 +843,8 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
   if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
   if (want == "explicit") { use_heap = false; use_compact = false; }
+  // categorical splits are evaluated by the explicit kernel only
+  if (f->has_cat) { use_heap = false; use_compact = false; }
   if (use_compact) {
     f->h_cpt_depth.assign(depth.begin(), depth.end());
     if (f->accum == TI_F64) {
@@ -872,6 +900,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   f->h_heap_leaf_ids.clear(); f->h_heap_leaf_ids.shrink_to_fit();
   f->h_nodes.clear(); f->h_nodes.shrink_to_fit();
   f->h_thr64.clear(); f->h_thr64.shrink_to_fit();
+  f->h_cat_words.clear(); f->h_cat_words.shrink_to_fit();
   f->h_leaves.clear(); f->h_leaves.shrink_to_fit();
   for (auto& ci : f->cpt) {
     ci.img.clear();

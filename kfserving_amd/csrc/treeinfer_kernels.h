@@ -41,6 +41,7 @@ namespace ti {
 
 constexpr uint32_t kMetaNanLeft = 0x80000000u;
 constexpr uint32_t kMetaZeroFlip = 0x40000000u;
+constexpr uint32_t kMetaCat = 0x20000000u;        // explicit layout: categorical node
 constexpr uint32_t kMetaFeatMask = 0x00FFFFFFu;
 constexpr int kMaxGroups = 16;
 constexpr uint32_t kCptLeaf = 512u;       // compact child code >= 512: leaf (code - 512)
@@ -87,6 +88,7 @@ struct KArgs {
   const int64_t* leaf_base;       // [T]
   const void* leaves;             // [n_leaves * leaf_width] ACC
   const int32_t* exp_leaf_ids;    // [n_leaves]
+  const uint32_t* cat_words;      // categorical bitsets: [nwords, w0, w1, ...] per node
   // compact layout (LDS-staged irregular trees)
   const int64_t* cpt_off;         // [T+1] byte offset of each tree record in the image
   const int32_t* cpt_nint;        // [T] internal nodes per tree
@@ -129,6 +131,17 @@ __device__ __forceinline__ bool go_left(XT x, XT thr, uint32_t meta) {
   if (CHECK_NAN) left = left || ((x != x) && (int32_t)meta < 0);
   if (ZERO) left = left != ((x == XT(0)) && (meta & kMetaZeroFlip) != 0);
   return left;
+}
+
+// LightGBM Tree::CategoricalDecision: v = (int)x; NaN, x <= -1 and
+// x >= 2^31 (INT_MIN on the reference's x86) go right; otherwise left iff bit
+// v is inside the node's bitset and set.  `bs` points at [nwords, w0, w1 ...].
+__device__ __forceinline__ bool cat_left(const uint32_t* bs, double x) {
+  if (!(x > -1.0 && x < 2147483648.0)) return false;
+  const uint32_t v = static_cast<uint32_t>(x);
+  const uint32_t w = v >> 5;
+  if (w >= bs[0]) return false;
+  return (bs[1 + w] >> (v & 31u)) & 1u;
 }
 
 // One heap node from LDS in a single wide read (ds_read_b64 / ds_read_b128).
@@ -598,7 +611,10 @@ __global__ void __launch_bounds__(512) explicit_predict_kernel(const KArgs a) {
         } else {
           x = (int)f < a.n_cols ? zero_map(xrow[f], a.lgb_zero_map) : nan_value<XT>();
         }
-        const int32_t next = go_left<ZERO>(x, thr[q], nd[q].y) ? (int32_t)nd[q].z : (int32_t)nd[q].w;
+        bool l = go_left<ZERO>(x, thr[q], nd[q].y);
+        if (a.cat_words != nullptr && (nd[q].y & kMetaCat))   // uniform test, then rare branch
+          l = cat_left(a.cat_words + nd[q].x, (double)x);
+        const int32_t next = l ? (int32_t)nd[q].z : (int32_t)nd[q].w;
         c[q] = c[q] < 0 ? c[q] : next;
         active |= c[q] >= 0;
       }

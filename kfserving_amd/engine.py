@@ -20,7 +20,7 @@ import numpy as np
 
 from .forest import (Forest, OUT_LEAF, OUT_MARGIN, OUT_PREDICT, TI_F32, TI_F64, TI_I32)
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("TREEINFER_LIB", os.path.join(_LIB_DIR, "libtreeinfer.so"))
 
@@ -63,6 +63,10 @@ class _ForestDesc(ctypes.Structure):
         ("transform", ctypes.c_int32),
         ("reserved0", ctypes.c_int32),
         ("transform_param", ctypes.c_double),
+        ("n_cat_words", ctypes.c_int64),
+        ("cat_bits", ctypes.c_void_p),
+        ("cat_offset", ctypes.c_void_p),
+        ("cat_nwords", ctypes.c_void_p),
     ]
 
 
@@ -182,6 +186,11 @@ class DeviceForest:
         desc.average_divisor = float(f.average_divisor)
         desc.transform = int(f.transform)
         desc.transform_param = float(f.transform_param)
+        if f.cat_bits is not None:
+            desc.n_cat_words = int(f.cat_bits.shape[0])
+            desc.cat_bits = _ptr(f.cat_bits) if f.cat_bits.size else None
+            desc.cat_offset = _ptr(f.cat_offset)
+            desc.cat_nwords = _ptr(f.cat_nwords)
         dev_arr = (ctypes.c_int32 * len(devs))(*devs)
         handle = ctypes.c_void_p()
         _check(self._lib, self._lib.ti_forest_create(ctypes.byref(desc), dev_arr, len(devs),

@@ -26,6 +26,7 @@ TI_I32 = 2
 # node flags
 NODE_NAN_LEFT = 0x01
 NODE_ZERO_FLIP = 0x02
+NODE_CATEGORICAL = 0x04
 
 # transforms
 T_IDENTITY = 0
@@ -79,6 +80,11 @@ class Forest:
     transform: int = T_IDENTITY
     transform_param: float = 1.0
     input_dtype: int = TI_F32        # how the plugin feeds X (xgb/sk: f32, lgb: f64)
+    # categorical splits (LightGBM): node goes left iff bit trunc(x) is set in
+    # cat_bits[cat_offset[n] : cat_offset[n] + cat_nwords[n]]
+    cat_bits: Optional[np.ndarray] = None       # uint32 [W]
+    cat_offset: Optional[np.ndarray] = None     # int64 [N]
+    cat_nwords: Optional[np.ndarray] = None     # int32 [N]
     library: str = ""
     objective: str = ""
     feature_names: Optional[List[str]] = None
@@ -138,6 +144,13 @@ class Forest:
         internal = self.feature >= 0
         if np.any(self.feature[internal] >= self.n_features):
             raise ValueError("split feature index >= n_features")
+        cat = internal & ((self.flags & NODE_CATEGORICAL) != 0)
+        if cat.any():
+            if self.cat_bits is None or self.cat_offset is None or self.cat_nwords is None:
+                raise ValueError("categorical nodes without bitsets")
+            end = self.cat_offset[cat] + self.cat_nwords[cat]
+            if np.any(self.cat_offset[cat] < 0) or np.any(end > self.cat_bits.shape[0]):
+                raise ValueError("categorical bitset out of range")
 
     def contiguous(self) -> "Forest":
         """Return self with every array C-contiguous in the ABI's dtypes."""
@@ -152,7 +165,15 @@ class Forest:
         self.leaf_value = np.ascontiguousarray(
             np.asarray(self.leaf_value, dtype=np.float64).reshape(self.n_nodes, self.leaf_width))
         self.base_margin = np.ascontiguousarray(self.base_margin, dtype=np.float64)
+        if self.cat_bits is not None:
+            self.cat_bits = np.ascontiguousarray(self.cat_bits, dtype=np.uint32)
+            self.cat_offset = np.ascontiguousarray(self.cat_offset, dtype=np.int64)
+            self.cat_nwords = np.ascontiguousarray(self.cat_nwords, dtype=np.int32)
         return self
+
+    @property
+    def has_categorical(self) -> bool:
+        return bool(np.any((self.flags & NODE_CATEGORICAL) != 0))
 
     def output_width(self, kind: int) -> int:
         if kind == OUT_LEAF:

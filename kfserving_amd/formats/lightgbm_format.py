@@ -11,6 +11,12 @@ and ``GBDT::PredictRaw``): features read as float64; missing type None maps
 NaN to 0.0, Zero sends |x| <= 1e-35 to the default child, NaN sends NaN to the
 default child; otherwise left iff ``x <= threshold``; scores accumulated in
 float64 in tree order, tree t feeding class t mod num_tree_per_iteration.
+
+Categorical splits (``Tree::CategoricalDecision``, decision_type bit 0): the
+node's threshold indexes ``cat_boundaries``; the row goes left iff bit
+``(int)x`` is set in ``cat_threshold[cat_boundaries[c]:cat_boundaries[c+1]]``;
+NaN, negative and out-of-range values go right.  Bitsets are concatenated
+over the forest into ``Forest.cat_bits`` with per-node word offsets.
 """
 from __future__ import annotations
 
@@ -18,9 +24,9 @@ from typing import Dict, List
 
 import numpy as np
 
-from ..forest import (Forest, MISSING_NAN, MISSING_NONE, MISSING_ZERO, NODE_NAN_LEFT,
-                      NODE_ZERO_FLIP, TI_F64, T_EXP, T_IDENTITY, T_LOG1PEXP, T_SIGMOID,
-                      T_SIGNSQUARE, T_SOFTMAX, concat_trees)
+from ..forest import (Forest, MISSING_NAN, MISSING_NONE, MISSING_ZERO, NODE_CATEGORICAL,
+                      NODE_NAN_LEFT, NODE_ZERO_FLIP, TI_F64, T_EXP, T_IDENTITY, T_LOG1PEXP,
+                      T_SIGMOID, T_SIGNSQUARE, T_SOFTMAX, concat_trees)
 
 
 class LightGBMFormatError(ValueError):
@@ -68,14 +74,15 @@ def objective_transform(objective: str):
 
 
 def _node_flags(decision_type: np.ndarray, threshold: np.ndarray) -> np.ndarray:
-    if np.any(decision_type & 1):
-        raise LightGBMFormatError("categorical splits are not supported yet")
     default_left = (decision_type & 2) != 0
     missing = (decision_type >> 2) & 3
     zero_left = 0.0 <= threshold             # where a NaN->0 / zero input lands
     nan_left = np.where(missing == MISSING_NONE, zero_left, default_left)
     zero_flip = (missing == MISSING_ZERO) & (default_left != zero_left)
     flags = np.where(nan_left, NODE_NAN_LEFT, 0) | np.where(zero_flip, NODE_ZERO_FLIP, 0)
+    # categorical nodes: Tree::CategoricalDecision (NaN / negative -> right)
+    cat = (decision_type & 1) != 0
+    flags = np.where(cat, NODE_CATEGORICAL, flags)
     if np.any((missing != MISSING_NONE) & (missing != MISSING_ZERO) & (missing != MISSING_NAN)):
         raise LightGBMFormatError("unknown missing type")
     return flags.astype(np.uint8)
@@ -86,8 +93,6 @@ def _tree(block: Dict[str, str]) -> dict:
     leaf_value = _floats(block["leaf_value"])
     if leaf_value.shape[0] != num_leaves:
         raise LightGBMFormatError("leaf_value length != num_leaves")
-    if int(block.get("num_cat", "0")) > 0:
-        raise LightGBMFormatError("categorical splits are not supported yet")
     if block.get("is_linear", "0").strip() not in ("", "0"):
         raise LightGBMFormatError("linear trees are not supported")
     if num_leaves == 1:
@@ -108,6 +113,18 @@ def _tree(block: Dict[str, str]) -> dict:
     # canonical numbering: internal nodes 0..n_int-1, leaf j at n_int + j
     left = np.where(lc >= 0, lc, n_int + ~lc)
     right = np.where(rc >= 0, rc, n_int + ~rc)
+    cat_off = np.full(n, -1, dtype=np.int64)
+    cat_nw = np.zeros(n, dtype=np.int32)
+    cat_words = np.zeros(0, dtype=np.uint32)
+    if int(block.get("num_cat", "0")) > 0:
+        bounds = _ints(block["cat_boundaries"])
+        cat_words = np.array([int(v) for v in block["cat_threshold"].split()], dtype=np.uint32)
+        is_cat = (dt & 1) != 0
+        ci = thr[is_cat].astype(np.int64)
+        if ci.size and (ci.min() < 0 or ci.max() + 1 >= bounds.shape[0]):
+            raise LightGBMFormatError("categorical threshold index out of range")
+        cat_off[:n_int][is_cat] = bounds[ci]
+        cat_nw[:n_int][is_cat] = bounds[ci + 1] - bounds[ci]
     return {
         "feature": np.concatenate([feat, np.full(num_leaves, -1)]),
         "threshold": np.concatenate([thr, np.zeros(num_leaves)]),
@@ -116,6 +133,7 @@ def _tree(block: Dict[str, str]) -> dict:
         "right": np.concatenate([right, np.full(num_leaves, -1)]),
         "leaf_id": np.concatenate([np.full(n_int, -1), np.arange(num_leaves)]),
         "leaf_value": np.concatenate([np.zeros(n_int), leaf_value]).reshape(n, 1),
+        "cat_offset": cat_off, "cat_nwords": cat_nw, "cat_words": cat_words,
     }
 
 
@@ -150,6 +168,20 @@ def parse_lightgbm_text(text: str) -> Forest:
         raise LightGBMFormatError("model has no trees")
     trees = [_tree(b) for b in blocks]
     cat = concat_trees(trees, 1)
+    # concatenate per-tree bitsets; node offsets become global word offsets
+    cat_bits, cat_offset, cat_nwords = None, None, None
+    if any(t.get("cat_words") is not None and t["cat_words"].size for t in trees):
+        base, words, offs, nws = 0, [], [], []
+        for t in trees:
+            o = t["cat_offset"].copy()
+            o[o >= 0] += base
+            offs.append(o)
+            nws.append(t["cat_nwords"])
+            words.append(t["cat_words"])
+            base += t["cat_words"].size
+        cat_bits = np.concatenate(words).astype(np.uint32)
+        cat_offset = np.concatenate(offs)
+        cat_nwords = np.concatenate(nws).astype(np.int32)
     ntpi = int(header.get("num_tree_per_iteration", header.get("num_class", "1")))
     K = max(1, ntpi)
     n_features = int(header.get("max_feature_idx", "-1")) + 1
@@ -173,6 +205,7 @@ def parse_lightgbm_text(text: str) -> Forest:
         transform=transform, transform_param=tparam, input_dtype=TI_F64,
         library="lightgbm", objective=objective, feature_names=names,
         meta={"version": header.get("version", ""), "num_class": int(header.get("num_class", 1))},
+        cat_bits=cat_bits, cat_offset=cat_offset, cat_nwords=cat_nwords,
     ).contiguous()
 
 
@@ -204,7 +237,8 @@ def write_lightgbm_text(path: str, trees: List[dict], n_features: int, objective
         nl = len(t["leaf_value"])
         out.append(f"Tree={i}")
         out.append(f"num_leaves={nl}")
-        out.append("num_cat=0")
+        cb = t.get("cat_boundaries")
+        out.append(f"num_cat={0 if cb is None else len(cb) - 1}")
         if nl > 1:
             out.append("split_feature=" + " ".join(str(int(v)) for v in t["split_feature"]))
             out.append("split_gain=" + " ".join("1" for _ in t["split_feature"]))
@@ -212,6 +246,9 @@ def write_lightgbm_text(path: str, trees: List[dict], n_features: int, objective
             out.append("decision_type=" + " ".join(str(int(v)) for v in t["decision_type"]))
             out.append("left_child=" + " ".join(str(int(v)) for v in t["left_child"]))
             out.append("right_child=" + " ".join(str(int(v)) for v in t["right_child"]))
+        if cb is not None and len(cb) > 1:
+            out.append("cat_boundaries=" + " ".join(str(int(v)) for v in cb))
+            out.append("cat_threshold=" + " ".join(str(int(v)) for v in t["cat_threshold"]))
         out.append("leaf_value=" + " ".join(_fmt(v) for v in t["leaf_value"]))
         out.append("shrinkage=1")
         out.append("")
@@ -220,6 +257,43 @@ def write_lightgbm_text(path: str, trees: List[dict], n_features: int, objective
     out.append("")
     with open(path, "w") as fh:
         fh.write("\n".join(out))
+
+
+def add_categorical_splits(trees: List[dict], cat_features, n_categories: int, seed: int,
+                           frac: float = 0.5) -> List[dict]:
+    """Turn a fraction of the splits on ``cat_features`` into categorical
+    splits (decision_type bit 0, threshold = index into cat_boundaries) with
+    random bitsets over ``n_categories`` values -- the shape lightgbm 2.3.1
+    writes (Tree::SplitCategorical): each bitset is just long enough for its
+    highest category."""
+    rng = np.random.default_rng(seed)
+    cat_features = np.asarray(cat_features)
+    for t in trees:
+        if len(t["leaf_value"]) <= 1:
+            continue
+        feat = np.asarray(t["split_feature"]).copy()
+        thr = np.asarray(t["threshold"], dtype=np.float64).copy()
+        dt = np.asarray(t["decision_type"]).copy()
+        bounds, words = [0], []
+        for i in range(feat.shape[0]):
+            if rng.random() >= frac:
+                continue
+            feat[i] = cat_features[rng.integers(0, cat_features.shape[0])]
+            members = np.nonzero(rng.random(n_categories) < 0.4)[0]
+            if members.size == 0:
+                members = np.array([int(rng.integers(0, n_categories))])
+            nw = int(members.max()) // 32 + 1
+            bits = np.zeros(nw, dtype=np.uint64)
+            for m in members:
+                bits[m // 32] |= np.uint64(1) << np.uint64(m % 32)
+            thr[i] = len(bounds) - 1
+            dt[i] = 1 | (int(dt[i]) & 2) | (int(rng.integers(0, 3)) << 2)
+            words.extend(int(w) for w in bits)
+            bounds.append(bounds[-1] + nw)
+        if len(bounds) > 1:
+            t.update(split_feature=feat, threshold=thr, decision_type=dt,
+                     cat_boundaries=np.asarray(bounds), cat_threshold=np.asarray(words))
+    return trees
 
 
 def synthetic_leafwise_trees(n_trees: int, num_leaves: int, n_features: int, seed: int,

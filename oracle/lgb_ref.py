@@ -10,6 +10,11 @@ Follows python/lgbserver/lgbserver/model.py:44-54 (one DataFrame per
   leaf_value (fixture python/lgbserver/lgbserver/example_model/model/model.bst:1-28).
 * predictor.hpp: a dense row keeps entries with |x| > kZeroThreshold (1e-35f)
   or NaN, everything else reads 0.0.
+* tree.h Tree::CategoricalDecision (decision_type bit 0): int_fval =
+  static_cast<int>(fval) -- on x86 a NaN or out-of-range value converts to
+  INT_MIN, so it goes right like any negative value; otherwise left iff bit
+  int_fval is set in the node's bitset cat_threshold[cat_boundaries[c] ..
+  cat_boundaries[c+1]) with c = (int)threshold (Common::FindInBitset).
 * tree.h Tree::NumericalDecision: missing type = (decision_type >> 2) & 3;
   NaN with type != NaN becomes 0.0; (Zero and IsZero(x)) or (NaN and isnan(x))
   -> default child (decision_type bit 1 = default left); else x <= threshold.
@@ -36,6 +41,8 @@ class LGBRefTree:
     left_child: np.ndarray
     right_child: np.ndarray
     leaf_value: np.ndarray
+    cat_boundaries: np.ndarray = None
+    cat_threshold: np.ndarray = None
 
 
 @dataclass
@@ -96,7 +103,27 @@ def _tree(b: Dict[str, str]) -> LGBRefTree:
         return np.array([float(x) for x in b.get(k, "").split()], dtype=np.float64)
 
     return LGBRefTree(nl, ints("split_feature"), flts("threshold"), ints("decision_type"),
-                      ints("left_child"), ints("right_child"), flts("leaf_value"))
+                      ints("left_child"), ints("right_child"), flts("leaf_value"),
+                      ints("cat_boundaries"), ints("cat_threshold").astype(np.uint32))
+
+
+def x86_int(fval: np.ndarray) -> np.ndarray:
+    """static_cast<int>(double) as cvttsd2si computes it: truncation, and
+    INT_MIN for NaN or anything outside the int range."""
+    fval = np.asarray(fval, dtype=np.float64)
+    bad = np.isnan(fval) | (fval >= 2147483648.0) | (fval <= -2147483649.0)
+    return np.where(bad, np.iinfo(np.int32).min, np.trunc(np.where(bad, 0, fval))).astype(np.int64)
+
+
+def categorical_left(tr: LGBRefTree, node: np.ndarray, fval: np.ndarray) -> np.ndarray:
+    iv = x86_int(fval)
+    c = tr.threshold[node].astype(np.int64)
+    lo = tr.cat_boundaries[c]
+    nw = tr.cat_boundaries[c + 1] - lo
+    word = np.where(iv >= 0, iv // 32, 0)
+    ok = (iv >= 0) & (word < nw)
+    w = tr.cat_threshold[np.where(ok, lo + word, 0)].astype(np.int64)
+    return ok & (((w >> np.where(ok, iv % 32, 0)) & 1) == 1)
 
 
 def from_raw_trees(trees, n_features: int, objective: str, num_class: int = 1) -> LGBRefModel:
@@ -108,7 +135,9 @@ def from_raw_trees(trees, n_features: int, objective: str, num_class: int = 1) -
                      np.asarray(t["threshold"], np.float64),
                      np.asarray(t["decision_type"], np.int64),
                      np.asarray(t["left_child"], np.int64), np.asarray(t["right_child"], np.int64),
-                     np.asarray(t["leaf_value"], np.float64)) for t in trees]
+                     np.asarray(t["leaf_value"], np.float64),
+                     np.asarray(t.get("cat_boundaries", []), np.int64),
+                     np.asarray(t.get("cat_threshold", []), np.uint32)) for t in trees]
     return LGBRefModel(header, False, rt)
 
 
@@ -149,14 +178,17 @@ def leaf_index(model: LGBRefModel, X: np.ndarray) -> np.ndarray:
                 break
             idx = np.nonzero(act)[0]
             n = node[idx]
-            fval = X[idx, tr.split_feature[n]]
+            raw = X[idx, tr.split_feature[n]]
             dt = tr.decision_type[n]
             mt = (dt >> 2) & 3
-            fval = np.where(np.isnan(fval) & (mt != 2), 0.0, fval)
+            fval = np.where(np.isnan(raw) & (mt != 2), 0.0, raw)
             is_zero = (fval >= -K_ZERO_THRESHOLD) & (fval <= K_ZERO_THRESHOLD)
             to_default = ((mt == 1) & is_zero) | ((mt == 2) & np.isnan(fval))
             default_left = (dt & 2) != 0
             go_left = np.where(to_default, default_left, fval <= tr.threshold[n])
+            cat = (dt & 1) != 0
+            if cat.any():
+                go_left = np.where(cat, categorical_left(tr, n, raw), go_left)
             node[idx] = np.where(go_left, tr.left_child[n], tr.right_child[n])
         out[:, t] = ~node
     return out

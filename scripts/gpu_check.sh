@@ -15,7 +15,7 @@ step() {  # name timeout cmd...
   return $rc
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step gpu_tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+step gpu_tests 900 python -m pytest tests -m gpu -q --maxfail=10 -p no:cacheprovider -rf
 step bench 600 python bench.py --steps 20 --warmup 5
 if [ "${PROFILE:-0}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

@@ -4,9 +4,22 @@ encoding (thresholds, NaN / zero flags, leaf payloads, base, transform)
 reproduces the oracle, independently of the GPU kernels."""
 import numpy as np
 
-from kfserving_amd.forest import (NODE_NAN_LEFT, NODE_ZERO_FLIP, OUT_LEAF, OUT_MARGIN,
+from kfserving_amd.forest import (NODE_CATEGORICAL, NODE_NAN_LEFT, NODE_ZERO_FLIP, OUT_LEAF, OUT_MARGIN,
                                   T_ARGMAX, T_EXP, T_HINGE, T_IDENTITY, T_SIGMOID, T_SOFTMAX,
                                   TI_F32, round_down_f32)
+
+
+def cat_left(f, g, x):
+    """Categorical rule of the ABI: left iff bit trunc(x) of the node's bitset
+    is set; NaN, negatives and values outside int32 go right."""
+    x = np.asarray(x, dtype=np.float64)
+    bad = np.isnan(x) | (x >= 2147483648.0) | (x <= -2147483649.0)
+    iv = np.where(bad, -1, np.trunc(np.where(bad, 0, x))).astype(np.int64)
+    off = f.cat_offset[g] if f.cat_offset is not None else np.zeros_like(g)
+    nw = f.cat_nwords[g] if f.cat_nwords is not None else np.zeros_like(g)
+    ok = (iv >= 0) & (iv // 32 < nw)
+    w = f.cat_bits[np.where(ok, off + iv // 32, 0)].astype(np.int64) if ok.any() else 0
+    return ok & (((w >> np.where(ok, iv % 32, 0)) & 1) == 1)
 
 
 def leaves(f, X):
@@ -32,6 +45,9 @@ def leaves(f, X):
             left = np.where(np.isnan(x), (f.flags[g] & NODE_NAN_LEFT) != 0, left)
             flip = (x == 0) & ((f.flags[g] & NODE_ZERO_FLIP) != 0)
             left = np.where(flip, ~left, left)
+            cat = (f.flags[g] & NODE_CATEGORICAL) != 0
+            if cat.any():
+                left = np.where(cat, cat_left(f, g, x), left)
             node[idx] = np.where(left, f.left[g], f.right[g])
         out[:, t] = node
     return out

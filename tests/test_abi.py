@@ -64,7 +64,8 @@ def test_abi_constants_match_python():
     consts = dict(re.findall(r"#define (TI_\w+)\s+(0x[0-9a-fA-F]+|-?\d+)", src))
     v = lambda k: int(consts[k], 0)
     assert (v("TI_F32"), v("TI_F64"), v("TI_I32")) == (F.TI_F32, F.TI_F64, F.TI_I32)
-    assert (v("TI_NODE_NAN_LEFT"), v("TI_NODE_ZERO_FLIP")) == (F.NODE_NAN_LEFT, F.NODE_ZERO_FLIP)
+    assert (v("TI_NODE_NAN_LEFT"), v("TI_NODE_ZERO_FLIP"), v("TI_NODE_CATEGORICAL")) == \
+        (F.NODE_NAN_LEFT, F.NODE_ZERO_FLIP, F.NODE_CATEGORICAL)
     assert (v("TI_OUTPUT_MARGIN"), v("TI_OUTPUT_PREDICT"), v("TI_OUTPUT_LEAF")) == \
         (F.OUT_MARGIN, F.OUT_PREDICT, F.OUT_LEAF)
     for name in ("IDENTITY", "SIGMOID", "SOFTMAX", "ARGMAX", "HINGE", "EXP", "SIGNSQUARE",

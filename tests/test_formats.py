@@ -65,6 +65,56 @@ def test_lgb_synthetic_missing_types(golden):
     np.testing.assert_array_equal(canon_eval.predict(f, g["X"], OUT_LEAF), g["leaf"])
 
 
+CAT_KA_C = [1, 3, 3.7, 33, 33.99, 2, 0, -0.5, -1, 32, 64, float("nan"), 1e10, -1e10, 1e-36]
+CAT_KA_WANT = [10, 10, 10, 10, 10, 20, 20, 20, 20, 20, 20, 20, 20, 20, 20.]
+
+
+def test_lgb_categorical_known_answers(golden):
+    """Hand-computed Tree::CategoricalDecision answers: the bitset {1, 3, 33}
+    (words 0b1010, 0b10); trunc toward zero; NaN / negative / past-the-bitset
+    / out-of-int-range go right (to the numerical split on x <= 0.5,
+    default-left so NaN x goes left)."""
+    p = os.path.join(golden, "lgb_categorical_ka.txt")
+    f = load_lightgbm_model(p)
+    assert f.has_categorical and f.cat_bits.tolist() == [10, 2]
+    c = np.array(CAT_KA_C)
+    want = np.array(CAT_KA_WANT)
+    X = np.stack([c, np.zeros_like(c)], axis=1)
+    m = lgb_ref.read_lgb_text(p)
+    np.testing.assert_array_equal(lgb_ref.predict(m, X), want)
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_MARGIN), want)
+    X[:, 1] = 1.0
+    want2 = np.where(want == 10, 10, 30.)
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_MARGIN), want2)
+    np.testing.assert_array_equal(canon_eval.predict(f, X.astype(np.float32), OUT_MARGIN), want2)
+
+
+def test_lgb_categorical_synthetic_matches_oracle(tmp_path):
+    trees = lf.synthetic_leafwise_trees(30, 31, 12, seed=11)
+    lf.add_categorical_splits(trees, [0, 3, 7], n_categories=70, seed=12)
+    p = str(tmp_path / "model.txt")
+    lf.write_lightgbm_text(p, trees, 12, "multiclass num_class:3", num_class=3)
+    f = load_lightgbm_model(p)
+    m = lgb_ref.read_lgb_text(p)
+    assert f.has_categorical
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((3000, 12))
+    for j in (0, 3, 7):
+        X[:, j] = rng.integers(-3, 80, size=3000) + rng.choice([0, 0.25, 0.999], size=3000)
+        X[rng.random(3000) < 0.05, j] = np.nan
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_LEAF), lgb_ref.leaf_index(m, X))
+    np.testing.assert_array_equal(canon_eval.predict(f, X, OUT_MARGIN),
+                                  lgb_ref.predict(m, X, raw_score=True))
+
+
+def test_lgb_categorical_bad_index(golden, tmp_path):
+    p = tmp_path / "bad.txt"
+    text = open(os.path.join(golden, "lgb_categorical_ka.txt")).read()
+    p.write_text(text.replace("threshold=0 0.5", "threshold=1 0.5"))
+    with pytest.raises(lf.LightGBMFormatError):
+        load_lightgbm_model(str(p))
+
+
 def test_xgb_writers_roundtrip(tmp_path):
     trees, ti = xf.synthetic_complete_trees(12, 5, 10, seed=4, num_class=3)
     pb = str(tmp_path / "m.bst")

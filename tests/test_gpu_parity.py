@@ -127,6 +127,60 @@ def test_lgb_synthetic_golden(golden, tmp_path, dtype):
     assert np.array_equal(dev.predict(X, OUT_LEAF), leaf)
 
 
+# ------------------------------------------------- LightGBM categorical splits
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lgb_categorical_known_answers_gpu(golden, dtype):
+    """Hand-computed Tree::CategoricalDecision answers (tests/test_formats.py)."""
+    from tests.test_formats import CAT_KA_C, CAT_KA_WANT
+    f = load_lightgbm_model(os.path.join(golden, "lgb_categorical_ka.txt"))
+    c = np.array(CAT_KA_C)
+    want = np.array(CAT_KA_WANT)
+    dev = DeviceForest(f, [0])
+    assert dev.info()["layout"] == 1
+    for xval, w in ((0.0, want), (1.0, np.where(want == 10, 10, 30.))):
+        X = np.stack([c, np.full_like(c, xval)], axis=1).astype(dtype)
+        assert np.array_equal(dev.predict(X, OUT_MARGIN), w)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("layout", ["heap", "explicit"])
+def test_lgb_categorical_synthetic_gpu(tmp_path, dtype, layout):
+    trees = lf.synthetic_leafwise_trees(60, 31, 12, seed=21)
+    lf.add_categorical_splits(trees, [0, 3, 7], n_categories=300, seed=22)
+    p = str(tmp_path / "model.txt")
+    lf.write_lightgbm_text(p, trees, 12, "multiclass num_class:3", num_class=3)
+    f = load_lightgbm_model(p)
+    m = lgb_ref.read_lgb_text(p)
+    rng = np.random.default_rng(23)
+    n = 5000
+    X = rng.standard_normal((n, 12))
+    for j in (0, 3, 7):
+        X[:, j] = rng.integers(-5, 320, size=n) + rng.choice([0, 0.5, 0.999], size=n)
+        X[rng.random(n) < 0.05, j] = np.nan
+        X[rng.random(n) < 0.01, j] = 3e9
+    X = X.astype(dtype)
+    dev = _dev_with_layout(f, layout)   # categorical forests always run explicit
+    assert dev.info()["layout"] == 1
+    Xd = X.astype(np.float64)
+    assert np.array_equal(dev.predict(X, OUT_LEAF), lgb_ref.leaf_index(m, Xd))
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), lgb_ref.predict(m, Xd, raw_score=True))
+    np.testing.assert_allclose(dev.predict(X, OUT_PREDICT), lgb_ref.predict(m, Xd), rtol=RTOL)
+
+
+def test_lgbserver_categorical_plugin(tmp_path):
+    from kfserving_amd.lgbserver import LightGBMModel
+    trees = lf.synthetic_leafwise_trees(10, 15, 4, seed=31)
+    lf.add_categorical_splits(trees, [1], n_categories=40, seed=32)
+    lf.write_lightgbm_text(str(tmp_path / "model.bst"), trees, 4, "binary sigmoid:1",
+                           feature_names=["a", "cat", "b", "c"])
+    model = LightGBMModel("m", str(tmp_path), 1)
+    model.load()
+    req = {"a": {0: 0.3, 1: -1.0}, "cat": {0: 7, 1: 12}, "b": {0: 0.0, 1: 2.0}, "c": {0: 1.0, 1: 0.5}}
+    got = model.predict({"inputs": [req]})["predictions"]
+    m = lgb_ref.read_lgb_text(str(tmp_path / "model.bst"))
+    np.testing.assert_allclose(got, lgb_ref.predict(m, lgb_ref.rows_from_inputs(m, [req])), rtol=RTOL)
+
+
 def test_sklearn_goldens_bit_exact(golden):
     f = load_tree_arrays(os.path.join(golden, "sk_rf_reg_model.npz"))
     g = np.load(os.path.join(golden, "sk_rf_reg.npz"))
