@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 N_TREES, DEPTH, N_FEAT, ROWS = 500, 8, 28, 1_000_000
 HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md)
+LAYOUT_NAMES = {0: "heap", 1: "explicit", 2: "compact", 3: "bheap"}
 
 
 def parse_args():
@@ -228,7 +229,8 @@ def main():
             try:
                 with open(args.traffic_json) as fh:
                     pmc = json.load(fh)
-                if pmc.get("rows") == rows and pmc.get("workload") == "c2":
+                if (pmc.get("rows") == rows and pmc.get("workload") == "c2"
+                        and pmc.get("layout", "heap") == LAYOUT_NAMES.get(info["layout"])):
                     traffic = pmc.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
@@ -260,8 +262,8 @@ def main():
             "config": {"workload": "C2 synthetic HIGGS-shaped XGBoost binary: 28 features, "
                                    "500 trees depth 8, 1M-row batch per GPU",
                        "rows_per_gpu": rows, "trees": N_TREES, "depth": DEPTH,
-                       "features": N_FEAT, "layout": "heap" if info["layout"] == 0 else
-                       "explicit", "parallelism": f"rows sharded x{world}"},
+                       "features": N_FEAT, "layout": LAYOUT_NAMES.get(info["layout"]),
+                       "parallelism": f"rows sharded x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "batched_latency": latency,

@@ -29,6 +29,7 @@
 
 #include "treeinfer.h"
 #include "treeinfer_kernels.h"
+#include "treeinfer_dispatch.h"
 
 using ti::ExpNode;
 using ti::HeapNode;
@@ -117,6 +118,9 @@ struct DeviceForest {
   int32_t* cpt_nint = nullptr;
   int32_t* cpt_depth = nullptr;
   int32_t* cpt_root = nullptr;
+  // binned heap layout: one image + threshold tables per input dtype
+  unsigned char* bh_img[2] = {nullptr, nullptr};
+  unsigned char* bh_tbl[2] = {nullptr, nullptr};
   // ti_predict scratch: device buffers + pinned host staging (grown x2)
   void* x_buf = nullptr;
   size_t x_cap = 0;
@@ -151,6 +155,17 @@ struct ti_forest {
     int64_t max_stage_bytes = 0;
   } cpt[2];
   std::vector<int32_t> h_cpt_nint, h_cpt_depth, h_cpt_root;
+  // binned heap layout (3): one image per input dtype (the ranks differ:
+  // float32 view round_down_f32(t), float64 view t)
+  struct BinImage {
+    std::vector<unsigned char> img;   // [T][stride]
+    std::vector<unsigned char> tbl;   // [F][2^L] XT Eytzinger tables
+    int32_t L = 0;
+    int32_t b16 = 1;
+    int32_t rows = 256;
+    int32_t words = 0;                // packed bin words per row
+    int64_t stride = 0;
+  } bh[2];
   // host images (kept until upload)
   std::vector<unsigned char> h_heap32, h_heap64;
   std::vector<int32_t> h_heap_leaf_ids;
@@ -183,7 +198,8 @@ void free_device(DeviceForest& d) {
   void* ptrs[] = {d.heap32, d.heap64, d.heap_leaf_ids, d.nodes, d.thr64, d.node_base, d.root,
                   d.leaf_base, d.leaves, d.exp_leaf_ids, d.tree_group, d.x_buf, d.out_buf,
                   d.cpt_img[0], d.cpt_img[1], d.cpt_off[0], d.cpt_off[1], d.cpt_stage[0],
-                  d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root, d.cat_words};
+                  d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root, d.cat_words,
+                  d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1]};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d.hx_pin) (void)hipHostFree(d.hx_pin);
@@ -204,6 +220,7 @@ void free_device(DeviceForest& d) {
   }
   d.cpt_nint = d.cpt_depth = d.cpt_root = nullptr;
   d.cat_words = nullptr;
+  for (int i = 0; i < 2; ++i) d.bh_img[i] = d.bh_tbl[i] = nullptr;
   d.x_cap = d.out_cap = 0;
   d.stream = nullptr;
   d.device = -1;
@@ -512,6 +529,114 @@ bool plan_compact(ti_forest* f, int idx, size_t xs) {
   return true;
 }
 
+// ------------------------------------------------------ binned heap packing
+// Rank binning (treeinfer_kernels.h, stage_bins): per feature the sorted
+// distinct thresholds of the XT view, an Eytzinger search table of 2^L
+// entries (1-based, +inf padded) and per-node ranks.  Returns false when the
+// forest does not qualify (too many distinct thresholds, or a feature image
+// whose offsets overflow the node's 15 bits even at 64-row tiles).
+template <typename XT>
+XT threshold_view(double t) {
+  if (sizeof(XT) == 4) return static_cast<XT>(round_down_f32(t));
+  return static_cast<XT>(t);
+}
+
+void eytzinger_fill(const std::vector<double>& sorted, std::vector<double>* out, size_t k, size_t* i) {
+  if (k >= out->size()) return;
+  eytzinger_fill(sorted, out, 2 * k, i);
+  (*out)[k] = *i < sorted.size() ? sorted[*i] : INFINITY;
+  ++*i;
+  eytzinger_fill(sorted, out, 2 * k + 1, i);
+}
+
+template <typename XT, typename ACC>
+bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
+                std::vector<int32_t>* leaf_ids) {
+  const int F = d->n_features;
+  const int LW = d->leaf_width;
+  std::vector<std::vector<XT>> u(F);
+  for (int64_t g = 0; g < d->n_nodes; ++g) {
+    if (d->feature[g] < 0 || (d->flags[g] & TI_NODE_CATEGORICAL)) continue;
+    const XT t = threshold_view<XT>(d->threshold[g]);
+    if (!std::isnan(static_cast<double>(t))) u[d->feature[g]].push_back(t);
+  }
+  size_t m_max = 0;
+  for (auto& v : u) {
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    m_max = std::max(m_max, v.size());
+  }
+  if (m_max > 65533) return false;
+  bi->b16 = m_max > 253 ? 1 : 0;
+  const int P = bi->b16 ? 2 : 4;
+  bi->words = (F + P - 1) / P;
+  int R = 256;
+  while (R > 64 && static_cast<int64_t>(bi->words) * R * 4 > static_cast<int64_t>(ti::kBNodeOffMask) + 1)
+    R >>= 1;
+  if (static_cast<int64_t>(bi->words) * R * 4 > static_cast<int64_t>(ti::kBNodeOffMask) + 1) return false;
+  bi->rows = R;
+  int L = 0;
+  while ((static_cast<size_t>(1) << L) - 1 < m_max) ++L;
+  bi->L = L;
+  const size_t tsz = static_cast<size_t>(1) << L;
+  bi->tbl.assign(static_cast<size_t>(F) * tsz * sizeof(XT), 0);
+  XT* tbl = reinterpret_cast<XT*>(bi->tbl.data());
+  std::vector<double> srt, ey(tsz);
+  for (int f = 0; f < F; ++f) {
+    srt.assign(u[f].begin(), u[f].end());
+    size_t i = 0;
+    std::fill(ey.begin(), ey.end(), static_cast<double>(INFINITY));
+    eytzinger_fill(srt, &ey, 1, &i);
+    for (size_t k = 0; k < tsz; ++k) tbl[f * tsz + k] = static_cast<XT>(ey[k]);
+  }
+  auto node_word = [&](int64_t g) -> uint32_t {
+    const int f = d->feature[g];
+    const XT t = threshold_view<XT>(d->threshold[g]);
+    uint32_t rank = 0;   // NaN threshold: never left
+    if (!std::isnan(static_cast<double>(t)))
+      rank = 1u + static_cast<uint32_t>(std::lower_bound(u[f].begin(), u[f].end(), t) - u[f].begin());
+    const uint32_t off = static_cast<uint32_t>((f / P) * R * 4 + (f % P) * (4 / P));
+    uint32_t w = off | (rank << 16);
+    if (d->flags[g] & TI_NODE_NAN_LEFT) w |= ti::kBNodeNanLeft;
+    return w;
+  };
+  const int NE = 1 << D;
+  bi->stride = static_cast<int64_t>(align16(sizeof(uint32_t) * NE + sizeof(ACC) * NE * LW));
+  bi->img.assign(static_cast<size_t>(bi->stride) * d->n_trees, 0);
+  if (leaf_ids) leaf_ids->assign(static_cast<size_t>(NE) * d->n_trees, 0);
+  struct Item { int32_t node; int32_t heap; int32_t level; };
+  std::vector<Item> st;
+  for (int t = 0; t < d->n_trees; ++t) {
+    unsigned char* rec = bi->img.data() + static_cast<size_t>(bi->stride) * t;
+    uint32_t* nodes = reinterpret_cast<uint32_t*>(rec);
+    ACC* leaves = reinterpret_cast<ACC*>(rec + sizeof(uint32_t) * NE);
+    const int64_t b = d->tree_offset[t];
+    st.assign(1, Item{0, 1, 0});
+    while (!st.empty()) {
+      const Item it = st.back();
+      st.pop_back();
+      const int64_t g = b + it.node;
+      if (it.level == D) {
+        const int slot = it.heap - NE;
+        for (int k = 0; k < LW; ++k)
+          leaves[static_cast<size_t>(slot) * LW + k] = static_cast<ACC>(d->leaf_value[g * LW + k]);
+        if (leaf_ids) (*leaf_ids)[static_cast<size_t>(t) * NE + slot] = d->leaf_id[g];
+        continue;
+      }
+      if (d->feature[g] < 0) {   // shallow leaf: always-left padding down to level D
+        nodes[it.heap] = 0xFFFFu << 16;
+        st.push_back(Item{it.node, 2 * it.heap, it.level + 1});
+        st.push_back(Item{it.node, 2 * it.heap + 1, it.level + 1});
+      } else {
+        nodes[it.heap] = node_word(g);
+        st.push_back(Item{d->left[g], 2 * it.heap, it.level + 1});
+        st.push_back(Item{d->right[g], 2 * it.heap + 1, it.level + 1});
+      }
+    }
+  }
+  return true;
+}
+
 int upload_device(ti_forest* f, DeviceForest& d, int device) {
   d.device = device;
   TI_HIP(hipSetDevice(device));
@@ -521,6 +646,12 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
   if (f->layout == 0) {
     if ((rc = upload(&d.heap32, f->h_heap32, &d.bytes))) return rc;
     if ((rc = upload(&d.heap64, f->h_heap64, &d.bytes))) return rc;
+    if ((rc = upload(&d.heap_leaf_ids, f->h_heap_leaf_ids, &d.bytes))) return rc;
+  } else if (f->layout == 3) {
+    for (int i = 0; i < 2; ++i) {
+      if ((rc = upload(&d.bh_img[i], f->bh[i].img, &d.bytes))) return rc;
+      if ((rc = upload(&d.bh_tbl[i], f->bh[i].tbl, &d.bytes))) return rc;
+    }
     if ((rc = upload(&d.heap_leaf_ids, f->h_heap_leaf_ids, &d.bytes))) return rc;
   } else if (f->layout == 2) {
     for (int i = 0; i < 2; ++i) {
@@ -549,42 +680,22 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
 }
 
 // ----------------------------------------------------------------- launch
-using KernelFn = void (*)(KArgs);
+using ti::KernelFn;
 
-template <typename XT, typename ACC, int KMAX, bool FL, bool Z>
-KernelFn pick_kernel(int layout) {
-  if (layout == 0) return ti::heap_predict_kernel<XT, ACC, KMAX, FL, Z>;
-  if (layout == 2) return ti::compact_predict_kernel<XT, ACC, KMAX, FL, Z>;
-  return ti::explicit_predict_kernel<XT, ACC, KMAX, FL, Z>;
-}
-
-// the LightGBM zero rule exists only for float64-accumulating forests
-template <typename XT, typename ACC, int KMAX, bool FL>
-KernelFn pick_kernel_z(int layout, bool z) {
-  if constexpr (sizeof(ACC) == 8) {
-    if (z) return pick_kernel<XT, ACC, KMAX, FL, true>(layout);
-  }
-  return pick_kernel<XT, ACC, KMAX, FL, false>(layout);
-}
-
-template <typename XT, typename ACC, int KMAX>
-KernelFn pick_kernel_fl(int layout, bool fl, bool z) {
-  return fl ? pick_kernel_z<XT, ACC, KMAX, true>(layout, z)
-            : pick_kernel_z<XT, ACC, KMAX, false>(layout, z);
-}
-
-template <typename XT, typename ACC>
-KernelFn pick_kernel_k(int layout, int K, bool fl, bool z) {
-  if (K == 1) return pick_kernel_fl<XT, ACC, 1>(layout, fl, z);
-  if (K <= 4) return pick_kernel_fl<XT, ACC, 4>(layout, fl, z);
-  return pick_kernel_fl<XT, ACC, 16>(layout, fl, z);
-}
-
+// Kernel instantiations live in one translation unit per (input, accumulator)
+// type pair (treeinfer_k_*.hip, compiled in parallel); see treeinfer_dispatch.h.
 KernelFn select_kernel(int layout, int xdt, int accum, int K, bool fl, bool z) {
-  if (xdt == TI_F32 && accum == TI_F32) return pick_kernel_k<float, float>(layout, K, fl, z);
-  if (xdt == TI_F32 && accum == TI_F64) return pick_kernel_k<float, double>(layout, K, fl, z);
-  if (xdt == TI_F64 && accum == TI_F64) return pick_kernel_k<double, double>(layout, K, fl, z);
-  return pick_kernel_k<double, float>(layout, K, fl, z);
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(layout, K, fl, z, false, 0);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(layout, K, fl, z, false, 0);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(layout, K, fl, z, false, 0);
+  return ti::kernels_df(layout, K, fl, z, false, 0);
+}
+
+KernelFn select_bheap(int xdt, int accum, int K, bool b16, int pf) {
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(3, K, true, false, b16, pf);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(3, K, true, false, b16, pf);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(3, K, true, false, b16, pf);
+  return ti::kernels_df(3, K, true, false, b16, pf);
 }
 
 std::mutex g_attr_mu;
@@ -633,6 +744,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   } else if (f->layout == 2) {
     const ti_forest::CptImage& ci = f->cpt[xdt == TI_F64 ? 1 : 0];
     R = ci.feat_lds ? ci.rows : 0;
+  } else if (f->layout == 3) {
+    R = f->bh[xdt == TI_F64 ? 1 : 0].rows;
   } else {
     R = 256;
     while (R > 64 && static_cast<size_t>(f->F) * R * xs > kFeatLdsMax) R >>= 1;
@@ -640,7 +753,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   }
   const bool feat_lds = R > 0;
   if (!feat_lds) R = 256;
-  const size_t feat_bytes = feat_lds ? align16(static_cast<size_t>(f->F) * R * xs) : 0;
+  size_t feat_bytes = feat_lds ? align16(static_cast<size_t>(f->F) * R * xs) : 0;
+  if (f->layout == 3) feat_bytes = static_cast<size_t>(f->bh[xdt == TI_F64 ? 1 : 0].words) * R * 4;
 
   KArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -697,6 +811,49 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     S = std::min<int64_t>(S, f->T);
     a.stage_trees = static_cast<int32_t>(S);
     lds = fixed + static_cast<size_t>(S * stride_b);
+  } else if (f->layout == 3) {
+    // binned heap: [bin image][flag][stage area = S tree records, also the
+    // binning temp of >= 8 columns].  S as for the heap layout: the most
+    // trees that keep the best workgroups-per-CU count, capped by the
+    // prefetch registers (PF x 16 B x R).
+    const int ii = xdt == TI_F64 ? 1 : 0;
+    const ti_forest::BinImage& bi = f->bh[ii];
+    const int64_t stride_b = bi.stride;
+    const size_t fixed = align16(feat_bytes + 4);
+    const size_t temp_min = 8 * static_cast<size_t>(R) * xs;
+    auto area = [&](int64_t n) { return std::max(static_cast<size_t>(n * stride_b), temp_min); };
+    auto wgs = [&](int64_t n) { return kLdsPerCu / (fixed + area(n)); };
+    const int64_t cap = static_cast<int64_t>(8) * 16 * R / stride_b;
+    int64_t S = std::min<int64_t>(ti::kTilp, cap);
+    if (S < 1) return fail(TI_ERR_UNSUPPORTED, "binned heap tree record does not fit the stage");
+    const size_t best = wgs(S);
+    while (S + ti::kTilp <= cap && S + ti::kTilp <= f->T && wgs(S + ti::kTilp) >= best) S += ti::kTilp;
+    static const int force_s = env_int("TI_BHEAP_STAGE", 0);
+    if (force_s > 0) S = std::min<int64_t>(force_s, cap);
+    S = std::min<int64_t>(S, f->T);
+    const int pf = S * stride_b <= static_cast<int64_t>(4) * 16 * R ? 4 : 8;
+    a.X = X;
+    a.trees = d.bh_img[ii];
+    a.tree_stride = stride_b;
+    a.heap_leaf_ids = d.heap_leaf_ids;
+    a.depth = f->depth;
+    a.stage_trees = static_cast<int32_t>(S);
+    a.bin_tbl = d.bh_tbl[ii];
+    a.bin_L = bi.L;
+    a.bin_words = bi.words;
+    a.stage_off = static_cast<int32_t>(fixed);
+    const size_t ar = area(S);
+    a.bin_chunk = static_cast<int32_t>(std::min<size_t>((ar / (static_cast<size_t>(R) * xs)) & ~size_t(7),
+                                                        static_cast<size_t>(f->F + 7) & ~size_t(7)));
+    lds = fixed + ar;
+    KernelFn fn = select_bheap(xdt, f->accum, f->K, bi.b16 != 0, pf);
+    int rc = ensure_lds_attr(d.device, fn);
+    if (rc) return rc;
+    const int64_t grid = (rows + R - 1) / R;
+    if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    TI_HIP(hipGetLastError());
+    return TI_OK;
   } else if (f->layout == 2) {
     const int ii = xdt == TI_F64 ? 1 : 0;
     const ti_forest::CptImage& ci = f->cpt[ii];
@@ -856,7 +1013,27 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
     }
     if (!plan_compact(f.get(), 0, 4) || !plan_compact(f.get(), 1, 8)) use_compact = false;
   }
-  if (use_compact) {
+  // binned heap (rank-binned features, 4-byte nodes) for complete-able trees
+  // without LightGBM zero-missing or categorical splits; TI_FORCE_LAYOUT=heap
+  // keeps the float-compare heap kernel
+  bool use_bheap = use_heap && !use_compact && want != "heap" && f->zero_rule == 0 && D >= 1 &&
+                   env_int("TI_NO_BHEAP", 0) == 0;
+  if (use_bheap) {
+    bool ok;
+    if (f->accum == TI_F64)
+      ok = pack_bheap<float, double>(desc, D, &f->bh[0], &f->h_heap_leaf_ids) &&
+           pack_bheap<double, double>(desc, D, &f->bh[1], nullptr);
+    else
+      ok = pack_bheap<float, float>(desc, D, &f->bh[0], &f->h_heap_leaf_ids) &&
+           pack_bheap<double, float>(desc, D, &f->bh[1], nullptr);
+    if (!ok) {
+      use_bheap = false;
+      for (auto& bi : f->bh) bi = ti_forest::BinImage();
+    }
+  }
+  if (use_bheap) {
+    f->layout = 3;
+  } else if (use_compact) {
     f->layout = 2;
     pack_explicit<char>(desc, f.get(), /*leaf_ids_only=*/true);
   } else if (use_heap) {
@@ -906,6 +1083,12 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
     ci.img.clear();
     ci.img.shrink_to_fit();
   }
+  for (auto& bi : f->bh) {
+    bi.img.clear();
+    bi.img.shrink_to_fit();
+    bi.tbl.clear();
+    bi.tbl.shrink_to_fit();
+  }
   *out = f.release();
   return TI_OK;
 }
@@ -926,7 +1109,7 @@ int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
   info->n_features = f->F;
   info->n_devices = static_cast<int32_t>(f->devs.size());
   info->device_bytes = f->devs.empty() ? 0 : f->devs[0]->bytes;
-  info->tree_stride_bytes = f->layout == 0 ? f->stride32 : 0;
+  info->tree_stride_bytes = f->layout == 0 ? f->stride32 : f->layout == 3 ? f->bh[0].stride : 0;
   return TI_OK;
 }
 

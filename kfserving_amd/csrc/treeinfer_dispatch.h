@@ -1,0 +1,54 @@
+// treeinfer_dispatch.h — kernel selection across the per-type translation
+// units.  Each treeinfer_k_<x><a>.hip instantiates every kernel of one
+// (input type, accumulator type) pair, so the four compile in parallel.
+#pragma once
+
+#include "treeinfer_kernels.h"
+
+namespace ti {
+
+using KernelFn = void (*)(KArgs);
+
+// layout: 0 heap, 1 explicit, 2 compact, 3 binned heap.  fl: feature image in
+// LDS; z: LightGBM zero rule; b16 / pf: binned heap bin width and prefetch
+// depth.
+template <typename XT, typename ACC, int KMAX>
+KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
+  if (layout == 3) {
+    if (b16) return pf <= 4 ? bheap_predict_kernel<XT, ACC, KMAX, true, 4>
+                            : bheap_predict_kernel<XT, ACC, KMAX, true, 8>;
+    return pf <= 4 ? bheap_predict_kernel<XT, ACC, KMAX, false, 4>
+                   : bheap_predict_kernel<XT, ACC, KMAX, false, 8>;
+  }
+  // the LightGBM zero rule exists only for float64-accumulating forests
+  if constexpr (sizeof(ACC) == 8) {
+    if (z) {
+      if (layout == 0) return fl ? heap_predict_kernel<XT, ACC, KMAX, true, true>
+                                 : heap_predict_kernel<XT, ACC, KMAX, false, true>;
+      if (layout == 2) return fl ? compact_predict_kernel<XT, ACC, KMAX, true, true>
+                                 : compact_predict_kernel<XT, ACC, KMAX, false, true>;
+      return fl ? explicit_predict_kernel<XT, ACC, KMAX, true, true>
+                : explicit_predict_kernel<XT, ACC, KMAX, false, true>;
+    }
+  }
+  if (layout == 0) return fl ? heap_predict_kernel<XT, ACC, KMAX, true, false>
+                             : heap_predict_kernel<XT, ACC, KMAX, false, false>;
+  if (layout == 2) return fl ? compact_predict_kernel<XT, ACC, KMAX, true, false>
+                             : compact_predict_kernel<XT, ACC, KMAX, false, false>;
+  return fl ? explicit_predict_kernel<XT, ACC, KMAX, true, false>
+            : explicit_predict_kernel<XT, ACC, KMAX, false, false>;
+}
+
+template <typename XT, typename ACC>
+KernelFn select_types(int layout, int K, bool fl, bool z, bool b16, int pf) {
+  if (K == 1) return select_layout<XT, ACC, 1>(layout, fl, z, b16, pf);
+  if (K <= 4) return select_layout<XT, ACC, 4>(layout, fl, z, b16, pf);
+  return select_layout<XT, ACC, 16>(layout, fl, z, b16, pf);
+}
+
+KernelFn kernels_ff(int layout, int K, bool fl, bool z, bool b16, int pf);   // float X, float acc
+KernelFn kernels_fd(int layout, int K, bool fl, bool z, bool b16, int pf);   // float X, double acc
+KernelFn kernels_dd(int layout, int K, bool fl, bool z, bool b16, int pf);   // double X, double acc
+KernelFn kernels_df(int layout, int K, bool fl, bool z, bool b16, int pf);   // double X, float acc
+
+}  // namespace ti

@@ -1,0 +1,8 @@
+// Kernel instantiations for input type double, accumulator type double.
+#include "treeinfer_dispatch.h"
+
+namespace ti {
+KernelFn kernels_dd(int layout, int K, bool fl, bool z, bool b16, int pf) {
+  return select_types<double, double>(layout, K, fl, z, b16, pf);
+}
+}  // namespace ti

@@ -97,6 +97,12 @@ struct KArgs {
   const int32_t* stage_start;     // [n_stages+1] first tree of each LDS stage
   int32_t n_stages;
   int32_t feat_shift;             // log2(R * sizeof(XT)): column stride of the LDS image
+  // binned layouts: rank images of the features (see stage_bins)
+  const void* bin_tbl;            // [F][2^bin_L] Eytzinger threshold tables, XT
+  int32_t bin_L;                  // search depth (common to all features)
+  int32_t bin_words;              // packed bin words per row (C)
+  int32_t bin_chunk;              // columns binned per pass through the temp area
+  int32_t stage_off;              // LDS byte offset of the tree stage / temp area
   // shared
   const int32_t* tree_group;      // [T]
   void* out;
@@ -429,6 +435,256 @@ __global__ void __launch_bounds__(512) heap_predict_kernel(const KArgs a) {
       heap_stage<XT, ACC, KMAX, FEAT_LDS, ZERO, true>(a, stage, cnt, t0, acc, lane_off, xrow, row, live);
     else
       heap_stage<XT, ACC, KMAX, FEAT_LDS, ZERO, false>(a, stage, cnt, t0, acc, lane_off, xrow, row, live);
+  }
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
+// ------------------------------------------------------- binned heap kernel
+// Rank binning.  For feature f let u_f[0] < ... < u_f[m-1] be the distinct
+// canonical thresholds (float32 view: round_down_f32(t); float64 view: t) of
+// all numerical splits on f.  A value x gets the bin b(x) = 1 + #{i : u_f[i] < x}
+// and the split on threshold u_f[k] gets the rank k + 1, so
+//     x <= u_f[k]   <=>   b(x) <= k + 1
+// for every non-NaN x, exactly.  NaN gets the code kBinNan (the largest
+// value of the bin width) and takes the node's NaN-left bit; a NaN threshold
+// (xgboost's t = -inf) has rank 0 (never left); a padding node has rank
+// 0xFFFF (always left, NaN included).  Bins are u16 (<= 65,533 thresholds
+// per feature) or u8 (<= 253), so the tile's feature image shrinks 2-4x and
+// more workgroups fit a CU -- which is what hides the LDS latency of the walk.
+//
+// The bin image in LDS is [word][R] of u32, each word packing P = 4/width
+// features of one row: feature f of lane l sits at byte
+//     (f / P) * R * 4 + l * 4 + (f % P) * width,
+// so the lanes of a read hit 32 distinct banks whatever feature each tests.
+// A binned heap node is one u32: bits 0..14 that byte offset minus the lane
+// part, bit 15 NaN-left, bits 16..31 the rank.
+constexpr uint32_t kBNodeNanLeft = 0x8000u;
+constexpr uint32_t kBNodeOffMask = 0x7FFFu;
+
+template <bool B16> struct BinTraits;
+template <> struct BinTraits<true> { static constexpr int P = 2; static constexpr uint32_t kNan = 0xFFFFu; };
+template <> struct BinTraits<false> { static constexpr int P = 4; static constexpr uint32_t kNan = 0xFFu; };
+
+template <bool B16, bool CHECK_NAN>
+__device__ __forceinline__ bool bin_left(uint32_t b, uint32_t nd) {
+  bool left = b <= (nd >> 16);
+  if (CHECK_NAN) left = left || (b == BinTraits<B16>::kNan && (nd & kBNodeNanLeft) != 0u);
+  return left;
+}
+
+template <bool B16>
+__device__ __forceinline__ uint32_t lds_bin(uint32_t byte_addr) {
+  if (B16)
+    return *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(
+        static_cast<uintptr_t>(byte_addr));
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(
+      static_cast<uintptr_t>(byte_addr));
+}
+
+// Bin the tile's rows into the LDS bin image (at LDS address 0).  Columns go
+// through `temp` (the tree-stage area, free at this point) bin_chunk at a
+// time: a coalesced copy into [c][R], then every lane searches its own row's
+// values in the Eytzinger tables (global, L2-resident: 2^L entries per
+// feature, node k's children 2k and 2k+1, padded with +inf), eight features
+// at once for eight independent load chains.  Returns (uniformly) whether a
+// live row of the tile holds a NaN.  Ends in a barrier.
+template <typename XT, bool B16>
+__device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const KArgs& a,
+                                           int64_t row0, int R, int tid) {
+  using BT = BinTraits<B16>;
+  constexpr int P = BT::P;
+  constexpr int Q = 8;   // features searched at once (a multiple of P)
+  const XT* X = static_cast<const XT*>(a.X);
+  const XT* tbl = static_cast<const XT*>(a.bin_tbl);
+  const int F = a.n_features;
+  const int C = a.n_cols;
+  const int L = a.bin_L;
+  const uint32_t tsz = 1u << L;
+  const int64_t left_rows = a.n_rows - row0;
+  const int rows_here = left_rows < R ? (int)left_rows : R;
+  bool has_nan = false;
+  if (tid == 0) *flag = 0;
+  for (int f0 = 0; f0 < F; f0 += a.bin_chunk) {
+    const int kc = (F - f0) < a.bin_chunk ? (F - f0) : a.bin_chunk;
+    __syncthreads();   // temp is free (the previous chunk is searched)
+    const uint32_t n = (uint32_t)rows_here * (uint32_t)kc;
+    const uint32_t ukc = (uint32_t)kc;
+    for (uint32_t e = tid; e < n; e += R) {
+      const uint32_t r = e / ukc;
+      const uint32_t c = e - r * ukc;
+      const int f = f0 + (int)c;
+      const XT v = f < C ? X[(row0 + r) * a.row_stride + f] : nan_value<XT>();
+      temp[c * R + r] = zero_map(v, a.lgb_zero_map);
+    }
+    __syncthreads();
+    for (int c = 0; c < kc; c += Q) {
+      XT x[Q];
+      const XT* tq[Q];
+      uint32_t k[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int cc = c + q < kc ? c + q : kc - 1;
+        x[q] = temp[cc * R + tid];
+        tq[q] = tbl + (size_t)(f0 + cc) * tsz;
+        k[q] = 1u;
+      }
+      for (int s = 0; s < L; ++s) {
+        XT e[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) e[q] = tq[q][k[q]];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
+      }
+      uint32_t w[Q / P];
+#pragma unroll
+      for (int j = 0; j < Q / P; ++j) w[j] = 0u;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const bool nan = x[q] != x[q];
+        has_nan |= nan && (c + q < kc);
+        const uint32_t b = nan ? BT::kNan : 1u + k[q] - tsz;
+        w[q / P] |= b << ((q % P) * (32 / P));
+      }
+#pragma unroll
+      for (int j = 0; j < Q / P; ++j) {
+        const int word = (f0 + c) / P + j;
+        if (c + j * P < kc) {
+          __attribute__((address_space(3))) uint32_t* dst =
+              reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+                  static_cast<uintptr_t>((uint32_t)(word * R + tid) * 4u));
+          *dst = w[j];
+        }
+      }
+    }
+  }
+  if (has_nan && tid < rows_here) *flag = 1;
+  __syncthreads();
+  return *flag != 0;
+}
+
+// Walk one LDS stage of binned complete trees.  A tree record is 2^D u32
+// entries (1-based heap: node i has children 2i and 2i+1; entry 0 unused),
+// then 2^D * leaf_width leaves (ACC).  At each level a lane issues the bin
+// read of its current node's feature AND the read of the node's two children
+// (one 8-byte word) together, so a level costs one LDS round trip, not two.
+template <typename ACC, int KMAX, bool B16, bool CHECK_NAN>
+__device__ __forceinline__ void bheap_stage(const KArgs& a, const unsigned char* stage, int cnt,
+                                            int t0, ACC (&acc)[KMAX], uint32_t lane_off,
+                                            int64_t row, bool live) {
+  const int D = a.depth;
+  const int NE = 1 << D;
+  const int T = a.n_trees;
+  const int64_t stride = a.tree_stride;
+  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
+  for (int j = 0; j < cnt; j += kTilp) {
+    const uint32_t* tp[kTilp];
+    uint32_t idx[kTilp], nd[kTilp];
+#pragma unroll
+    for (int q = 0; q < kTilp; ++q) {
+      const int tq = (j + q) < cnt ? (j + q) : (cnt - 1);
+      tp[q] = reinterpret_cast<const uint32_t*>(stage + (int64_t)tq * stride);
+      idx[q] = 1u;
+      nd[q] = tp[q][1];   // the root: one broadcast read
+    }
+    for (int l = 0; l + 1 < D; ++l) {
+      uint32_t b[kTilp];
+      uint2 pr[kTilp];
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q) {
+        b[q] = lds_bin<B16>((nd[q] & kBNodeOffMask) | lane_off);
+        pr[q] = *reinterpret_cast<const uint2*>(tp[q] + 2u * idx[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q) {
+        const bool left = bin_left<B16, CHECK_NAN>(b[q], nd[q]);
+        idx[q] = 2u * idx[q] + (left ? 0u : 1u);
+        nd[q] = left ? pr[q].x : pr[q].y;
+      }
+    }
+    {   // last level: the children are leaves
+      uint32_t b[kTilp];
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q) b[q] = lds_bin<B16>((nd[q] & kBNodeOffMask) | lane_off);
+#pragma unroll
+      for (int q = 0; q < kTilp; ++q)
+        idx[q] = 2u * idx[q] + (bin_left<B16, CHECK_NAN>(b[q], nd[q]) ? 0u : 1u);
+    }
+#pragma unroll
+    for (int q = 0; q < kTilp; ++q) {
+      if (j + q < cnt) {
+        const int leaf = (int)idx[q] - NE;
+        const int t = t0 + j + q;
+        if (want_leaf) {
+          if (live) static_cast<int32_t*>(a.out)[row * T + t] = a.heap_leaf_ids[(int64_t)t * NE + leaf];
+        } else {
+          const ACC* lv = reinterpret_cast<const ACC*>(tp[q] + NE);
+          add_leaf<ACC, KMAX>(acc, lv, leaf, a.leaf_width, a.tree_group[t]);
+        }
+      }
+    }
+  }
+}
+
+template <int PF>
+__device__ __forceinline__ void prefetch_n(u32x4 (&pf)[PF], const u32x4* __restrict__ src,
+                                           int n16, int tid, int R) {
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const int i = tid + u * R;
+    pf[u] = src[i < n16 ? i : n16 - 1];
+  }
+}
+template <int PF>
+__device__ __forceinline__ void commit_n(const u32x4 (&pf)[PF], u32x4* __restrict__ dst, int n16,
+                                         int tid, int R) {
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const int i = tid + u * R;
+    if (i < n16) dst[i] = pf[u];
+  }
+}
+
+// LDS: [bin image (bin_words * R u32)] [flag word] ... [stage area at
+// stage_off: S tree records, also the binning temp].
+template <typename XT, typename ACC, int KMAX, bool B16, int PF>
+__global__ void __launch_bounds__(256) bheap_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  unsigned char* stage = smem + a.stage_off;
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  const int T = a.n_trees;
+  const int S = a.stage_trees;
+  const int64_t stride = a.tree_stride;
+  // first stage in flight while the tile is binned
+  u32x4 pf[PF];
+  prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees),
+                 (int)(((int64_t)(T < S ? T : S) * stride) >> 4), tid, R);
+  const bool tile_nan = stage_bins<XT, B16>(flag, reinterpret_cast<XT*>(stage), a, row0, R, tid);
+
+  ACC acc[KMAX];
+  init_acc(acc, a);
+  const int last0 = ((T - 1) / S) * S;
+  for (int t0 = 0; t0 < T; t0 += S) {
+    const int cnt = (T - t0) < S ? (T - t0) : S;
+    __syncthreads();
+    commit_n<PF>(pf, reinterpret_cast<u32x4*>(stage), (int)(((int64_t)cnt * stride) >> 4), tid, R);
+    __syncthreads();
+    {
+      const int tn = t0 + S <= last0 ? t0 + S : last0;
+      const int cn = (T - tn) < S ? (T - tn) : S;
+      prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees + (int64_t)tn * stride),
+                     (int)(((int64_t)cn * stride) >> 4), tid, R);
+    }
+    if (tile_nan)
+      bheap_stage<ACC, KMAX, B16, true>(a, stage, cnt, t0, acc, lane_off, row, live);
+    else
+      bheap_stage<ACC, KMAX, B16, false>(a, stage, cnt, t0, acc, lane_off, row, live);
   }
   if (!live || a.kind == TI_OUTPUT_LEAF) return;
   finish_row<ACC, KMAX>(acc, a, row);

@@ -301,7 +301,7 @@ def test_c2_full_size_matches_c_port():
     Every margin bit-exact against the C/OpenMP restatement of xgboost 0.82."""
     trees, ti = xf.synthetic_complete_trees(500, 8, 28, seed=0)
     dev = DeviceForest(xf.forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic"), [0])
-    assert dev.info()["layout"] == 0 and dev.info()["depth"] == 8
+    assert dev.info()["layout"] in (0, 3) and dev.info()["depth"] == 8
     rng = np.random.default_rng(0)
     X = rng.standard_normal((1_000_000, 28), dtype=np.float32)
     X[rng.random(X.shape, dtype=np.float32) < 0.01] = np.nan
@@ -340,10 +340,10 @@ def _dev_with_layout(forest, layout):
             os.environ["TI_FORCE_LAYOUT"] = old
 
 
-LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2}
+LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2, "bheap": 3}
 
 
-@pytest.mark.parametrize("layout", ["heap", "compact", "explicit"])
+@pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit"])
 def test_xgb_golden_every_layout(golden, layout):
     g = np.load(os.path.join(golden, "xgb_synth.npz"))
     trees, ti = xf.synthetic_complete_trees(40, 8, 28, seed=1)
@@ -376,7 +376,7 @@ def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
     assert np.array_equal(dev.predict(X, OUT_LEAF), lgb_ref.leaf_index(lm, Xd))
 
 
-@pytest.mark.parametrize("layout", ["heap", "compact", "explicit"])
+@pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit"])
 def test_lgb_iris_fixture_every_layout(golden, layout):
     from sklearn.datasets import load_iris
     path = os.path.join(golden, "lgb_iris_v3.txt")
