@@ -824,10 +824,10 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     auto area = [&](int64_t n) { return std::max(static_cast<size_t>(n * stride_b), temp_min); };
     auto wgs = [&](int64_t n) { return kLdsPerCu / (fixed + area(n)); };
     const int64_t cap = static_cast<int64_t>(8) * 16 * R / stride_b;
-    int64_t S = std::min<int64_t>(ti::kTilp, cap);
+    int64_t S = std::min<int64_t>(ti::kBTilp, cap);
     if (S < 1) return fail(TI_ERR_UNSUPPORTED, "binned heap tree record does not fit the stage");
     const size_t best = wgs(S);
-    while (S + ti::kTilp <= cap && S + ti::kTilp <= f->T && wgs(S + ti::kTilp) >= best) S += ti::kTilp;
+    while (S + ti::kBTilp <= cap && S + ti::kBTilp <= f->T && wgs(S + ti::kBTilp) >= best) S += ti::kBTilp;
     static const int force_s = env_int("TI_BHEAP_STAGE", 0);
     if (force_s > 0) S = std::min<int64_t>(force_s, cap);
     S = std::min<int64_t>(S, f->T);

@@ -33,6 +33,12 @@
 #ifndef TI_TILP
 #define TI_TILP 8   // trees walked concurrently per lane (heap layout)
 #endif
+#ifndef TI_ASM_STEP
+#define TI_ASM_STEP 1   // binned heap: hand-scheduled compare/select/carry step
+#endif
+#ifndef TI_BTILP
+#define TI_BTILP 4      // trees walked concurrently per lane (binned heap)
+#endif
 #ifndef TI_PF
 #define TI_PF 8     // 16-byte words per thread prefetched for the next tree stage
 #endif
@@ -47,6 +53,7 @@ constexpr int kMaxGroups = 16;
 constexpr uint32_t kCptLeaf = 512u;       // compact child code >= 512: leaf (code - 512)
 constexpr int kExpIlp = 4;                // trees per lane in the global explicit kernel
 constexpr int kTilp = TI_TILP;
+constexpr int kBTilp = TI_BTILP;
 constexpr int kPf = TI_PF;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
 
@@ -577,41 +584,62 @@ __device__ __forceinline__ void bheap_stage(const KArgs& a, const unsigned char*
   const int T = a.n_trees;
   const int64_t stride = a.tree_stride;
   const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
-  for (int j = 0; j < cnt; j += kTilp) {
-    const uint32_t* tp[kTilp];
-    uint32_t idx[kTilp], nd[kTilp];
+  for (int j = 0; j < cnt; j += kBTilp) {
+    const uint32_t* tp[kBTilp];
+    uint32_t idx[kBTilp], nd[kBTilp];
 #pragma unroll
-    for (int q = 0; q < kTilp; ++q) {
+    for (int q = 0; q < kBTilp; ++q) {
       const int tq = (j + q) < cnt ? (j + q) : (cnt - 1);
       tp[q] = reinterpret_cast<const uint32_t*>(stage + (int64_t)tq * stride);
       idx[q] = 1u;
       nd[q] = tp[q][1];   // the root: one broadcast read
     }
     for (int l = 0; l + 1 < D; ++l) {
-      uint32_t b[kTilp];
-      uint2 pr[kTilp];
+      uint32_t b[kBTilp];
+      uint2 pr[kBTilp];
 #pragma unroll
-      for (int q = 0; q < kTilp; ++q) {
+      for (int q = 0; q < kBTilp; ++q) {
         b[q] = lds_bin<B16>((nd[q] & kBNodeOffMask) | lane_off);
         pr[q] = *reinterpret_cast<const uint2*>(tp[q] + 2u * idx[q]);
       }
 #pragma unroll
-      for (int q = 0; q < kTilp; ++q) {
-        const bool left = bin_left<B16, CHECK_NAN>(b[q], nd[q]);
-        idx[q] = 2u * idx[q] + (left ? 0u : 1u);
-        nd[q] = left ? pr[q].x : pr[q].y;
+      for (int q = 0; q < kBTilp; ++q) {
+#if TI_ASM_STEP == 2
+        if (!CHECK_NAN) {
+          uint64_t m;
+          asm("v_cmp_lt_u32_sdwa %2, %0, %3 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+              "v_cndmask_b32_e64 %0, %4, %5, %2\n\t"
+              "v_addc_co_u32_e64 %1, %2, %1, %1, %2"
+              : "+v"(nd[q]), "+v"(idx[q]), "=&s"(m) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y));
+          continue;
+        }
+#elif TI_ASM_STEP
+        if (!CHECK_NAN) {
+          // right = rank < bin (SDWA compare on the node's high half), then the
+          // child select and idx = 2 idx + right as one carry-in add: 3 VALU
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %2 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+              "v_cndmask_b32 %0, %3, %4, vcc\n\t"
+              "v_addc_co_u32 %1, vcc, %1, %1, vcc"
+              : "+v"(nd[q]), "+v"(idx[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y)
+              : "vcc");
+          continue;
+        }
+#endif
+        const bool right = !bin_left<B16, CHECK_NAN>(b[q], nd[q]);
+        idx[q] = idx[q] + idx[q] + (uint32_t)right;
+        nd[q] = right ? pr[q].y : pr[q].x;
       }
     }
     {   // last level: the children are leaves
-      uint32_t b[kTilp];
+      uint32_t b[kBTilp];
 #pragma unroll
-      for (int q = 0; q < kTilp; ++q) b[q] = lds_bin<B16>((nd[q] & kBNodeOffMask) | lane_off);
+      for (int q = 0; q < kBTilp; ++q) b[q] = lds_bin<B16>((nd[q] & kBNodeOffMask) | lane_off);
 #pragma unroll
-      for (int q = 0; q < kTilp; ++q)
-        idx[q] = 2u * idx[q] + (bin_left<B16, CHECK_NAN>(b[q], nd[q]) ? 0u : 1u);
+      for (int q = 0; q < kBTilp; ++q)
+        idx[q] = idx[q] + idx[q] + (uint32_t)!bin_left<B16, CHECK_NAN>(b[q], nd[q]);
     }
 #pragma unroll
-    for (int q = 0; q < kTilp; ++q) {
+    for (int q = 0; q < kBTilp; ++q) {
       if (j + q < cnt) {
         const int leaf = (int)idx[q] - NE;
         const int t = t0 + j + q;

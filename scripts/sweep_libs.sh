@@ -1,13 +1,10 @@
 #!/bin/bash
-# A/B library builds (TREEINFER_LIB) on the C2 bench; interleaved rounds.
+# A/B the C2 bench across variant libraries (scripts/build_variant.sh).
+# Usage: scripts/sweep_libs.sh name1 name2 ...   ("default" = the in-tree build)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for round in 1 2; do
-  for lib in ${LIBS:-libtreeinfer.so}; do
-    out=$(TREEINFER_LIB=$PWD/kfserving_amd/lib/$lib timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu-baseline 2>/dev/null | tail -1)
-    rc=$?
-    echo "round=$round lib=$lib $(echo "$out" | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print("%.3e rows/s  kernel %.3f ms" % (d["value"], d["roofline"]["kernel_ms"]))' 2>/dev/null)" | tee -a gpurun_out/sweep_libs.log
-    [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
-  done
+for n in "$@"; do
+  if [ "$n" = default ]; then lib=kfserving_amd/lib/libtreeinfer.so; else lib=kfserving_amd/lib/variants/libtreeinfer_$n.so; fi
+  r=$(timeout -k 10 120 env TREEINFER_LIB=$lib ${SWEEP_ENV} python bench.py --steps 20 --warmup 5 --no-cpu-baseline --latency-qps 0 2>/dev/null | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("%.4e rows/s kernel %.4f ms layout %s" % (d["value"], d["roofline"]["kernel_ms"], d["config"]["layout"]))')
+  echo "$n ${SWEEP_ENV} :: $r" | tee -a gpurun_out/sweep.log
 done
-exit 0
