@@ -676,7 +676,7 @@ __device__ __forceinline__ void commit_n(const u32x4 (&pf)[PF], u32x4* __restric
 // LDS: [bin image (bin_words * R u32)] [flag word] ... [stage area at
 // stage_off: S tree records, also the binning temp].
 template <typename XT, typename ACC, int KMAX, bool B16, int PF>
-__global__ void __launch_bounds__(256) bheap_predict_kernel(const KArgs a) {
+__global__ void __launch_bounds__(512) bheap_predict_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int R = blockDim.x;
   const int tid = threadIdx.x;
