@@ -1,0 +1,43 @@
+/*
+ * kfserve.h — native host-side helpers of the KFServing v1 serving path
+ * (libkfserve.so, built from kfserving_amd/csrc/kfserve_host.cpp).
+ *
+ * The reference decodes every request body with tornado's json_decode and
+ * builds the library's input from Python lists:
+ *   python/kfserving/kfserving/handlers/http.py:69   json.loads(self.request.body)
+ *   python/xgbserver/xgbserver/model.py:46          xgb.DMatrix(request["instances"])
+ *   python/sklearnserver/sklearnserver/model.py:46  np.array(instances)
+ * which costs ~1e5 rows/s per core at 28 features.  This
+ * parser turns the common body shape straight into a float64 row-major
+ * matrix.  It is exact: every number becomes the double that Python's
+ * float(text) (correctly rounded) would give, so the matrix equals
+ * np.asarray(json.loads(body)["instances"], dtype=np.float64).
+ */
+#ifndef KFSERVE_H_
+#define KFSERVE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KF_PARSED      1   /* fast path taken: out[0 .. rows*cols) filled          */
+#define KF_FALLBACK    0   /* body outside the fast subset (or malformed): use a   */
+                           /* general JSON parser, which also reports the error    */
+#define KF_ERR_SPACE  -1   /* out too small: need *rows * *cols elements           */
+
+/* Parse a v1 request body of exactly the shape {"instances": [[n, n, ...], ...]}
+ * (any whitespace; one top-level key; rows of equal, non-zero length; numbers
+ * in JSON syntax plus Python's NaN / Infinity / -Infinity literals).  Anything
+ * else -- other keys, strings, true/false/null, nested or ragged rows,
+ * integers with more than 18 digits, trailing bytes -- returns KF_FALLBACK so
+ * that the caller's json.loads path keeps the reference's exact behaviour. */
+int kf_parse_instances(const char* body, int64_t len, double* out, int64_t cap,
+                       int64_t* rows, int64_t* cols);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* KFSERVE_H_ */

@@ -27,7 +27,10 @@ import time
 import uuid
 from typing import Any, Awaitable, Callable, Dict, List, Optional, Tuple
 
+import numpy as np
+
 from ..kfserving.errors import HTTPError
+from ..kfserving.fastjson import JsonInstances
 
 MAX_BATCH_SIZE = 32       # handler.go:34
 MAX_LATENCY_MS = 5000     # handler.go:35
@@ -47,7 +50,8 @@ class Batcher:
         self.predict_batch = predict_batch
         self.pipeline = pipeline
         self._sem = asyncio.Semaphore(max_inflight if pipeline else 1)
-        self._instances: List[Any] = []
+        self._instances: List[Any] = []   # one chunk (list or matrix) per request
+        self._rows = 0
         self._waiters: List[Tuple[asyncio.Future, int, int]] = []
         self._start = 0.0
         self._timer: Optional[asyncio.TimerHandle] = None
@@ -55,16 +59,22 @@ class Batcher:
         self.stats = {"batches": 0, "rows": 0, "max_batch_rows": 0}
 
     async def submit(self, instances: List[Any]) -> Dict[str, Any]:
-        if not isinstance(instances, list) or len(instances) == 0:
+        """Queue one request's rows: a list, or a 2-D matrix decoded natively
+        from the body (kfserving.fastjson.JsonInstances)."""
+        if isinstance(instances, np.ndarray):
+            if instances.ndim != 2 or instances.shape[0] == 0:
+                raise HTTPError(400, "no instances in the request")
+        elif not isinstance(instances, list) or len(instances) == 0:
             raise HTTPError(400, "no instances in the request")
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         if not self._instances:
             self._start = time.monotonic()
-        lo = len(self._instances)
-        self._instances.extend(instances)
-        self._waiters.append((fut, lo, len(self._instances)))
-        if len(self._instances) >= self.max_batch_size:
+        lo = self._rows
+        self._instances.append(instances)
+        self._rows += len(instances)
+        self._waiters.append((fut, lo, self._rows))
+        if self._rows >= self.max_batch_size:
             self._flush()
         elif self._timer is None:
             delay = self.max_latency_ms / 1000.0 - (time.monotonic() - self._start)
@@ -77,8 +87,8 @@ class Batcher:
             self._timer = None
         if not self._instances:
             return
-        batch, waiters = self._instances, self._waiters
-        self._instances, self._waiters = [], []
+        batch, waiters = _combine(self._instances), self._waiters
+        self._instances, self._waiters, self._rows = [], [], 0
         self.stats["batches"] += 1
         self.stats["rows"] += len(batch)
         self.stats["max_batch_rows"] = max(self.stats["max_batch_rows"], len(batch))
@@ -112,6 +122,22 @@ class Batcher:
         self._flush()
         while self._tasks:
             await asyncio.gather(*list(self._tasks))
+
+
+def _combine(chunks: List[Any]):
+    """One batch from the queued requests: matrices of equal width are
+    concatenated (keeping the JsonInstances marker when every chunk has it);
+    anything else becomes one list of rows, as the Go batcher appends them."""
+    if all(isinstance(c, np.ndarray) for c in chunks) and \
+            len({c.shape[1] for c in chunks}) == 1:
+        out = np.concatenate(chunks, axis=0) if len(chunks) > 1 else chunks[0]
+        if all(isinstance(c, JsonInstances) for c in chunks):
+            return out.view(JsonInstances)
+        return np.asarray(out)
+    rows: List[Any] = []
+    for c in chunks:
+        rows.extend(c.tolist() if isinstance(c, np.ndarray) else c)
+    return rows
 
 
 class ModelBatcher(Batcher):

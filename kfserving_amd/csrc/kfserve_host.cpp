@@ -1,0 +1,309 @@
+// kfserve_host.cpp — libkfserve.so: native v1 request-body parser
+// (include/kfserve.h).  Host code only; no GPU.
+//
+// Replaces, for the common body shape, the json.loads + list -> ndarray
+// conversion of the reference serving path (handlers/http.py:69,
+// xgbserver/model.py:46, sklearnserver/model.py:46).  Exactness: a number
+// with a decimal significand w < 2^53 and a power of ten 10^e, |e| <= 22, is
+// one correctly rounded IEEE operation w * 10^e or w / 10^-e (Clinger's fast
+// path); every other number goes to strtod, which is correctly rounded in
+// glibc -- the same result as Python's float(text); significands of at most
+// 19 digits take the Eisel-Lemire conversion instead (exact, ~10x faster).  Integer literals of up
+// to 18 digits convert exactly as Python's int -> float (round to nearest
+// even), which is what numpy does with them.
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "kfserve.h"
+#include "pow5_table.h"
+
+namespace {
+
+// Eisel-Lemire (Lemire 2021, as in the fast_float library): the correctly
+// rounded binary64 nearest to w * 10^q for a nonzero decimal significand w
+// of at most 19 digits, q in [-342, 308], from one or two 64x128-bit
+// products with the truncated power of five.  Mushtak & Lemire (2023) show
+// the result needs no fallback for such w.
+double eisel_lemire(uint64_t w, int64_t q, bool neg) {
+  const uint64_t sign = neg ? (uint64_t(1) << 63) : 0;
+  auto bits = [&](uint64_t m, int64_t p2) {
+    const uint64_t b = sign | (static_cast<uint64_t>(p2) << 52) | m;
+    double d;
+    std::memcpy(&d, &b, 8);
+    return d;
+  };
+  if (w == 0 || q < -342) return bits(0, 0);
+  if (q > 308) return bits(0, 0x7FF);
+  const int lz = __builtin_clzll(w);
+  w <<= lz;
+  const int idx = 2 * static_cast<int>(q + 342);
+  unsigned __int128 first = static_cast<unsigned __int128>(w) * kPow5_128[idx];
+  uint64_t hi = static_cast<uint64_t>(first >> 64), lo = static_cast<uint64_t>(first);
+  const uint64_t mask = 0xFFFFFFFFFFFFFFFFULL >> 55;   // 52 + 3 bits of precision
+  if ((hi & mask) == mask) {
+    const unsigned __int128 second = static_cast<unsigned __int128>(w) * kPow5_128[idx + 1];
+    const uint64_t shi = static_cast<uint64_t>(second >> 64);
+    lo += shi;
+    if (shi > lo) ++hi;
+  }
+  const int upper = static_cast<int>(hi >> 63);
+  const int shift = upper + 64 - 52 - 3;
+  uint64_t m = hi >> shift;
+  int64_t p2 = ((((152170 + 65536) * q) >> 16) + 63) + upper - lz + 1023;
+  if (p2 <= 0) {   // subnormal
+    if (-p2 + 1 >= 64) return bits(0, 0);
+    m >>= -p2 + 1;
+    m += (m & 1);
+    m >>= 1;
+    p2 = m < (uint64_t(1) << 52) ? 0 : 1;
+    return bits(m & ~(uint64_t(1) << 52), p2);
+  }
+  if (lo <= 1 && q >= -4 && q <= 23 && (m & 3) == 1 && (m << shift) == hi) m &= ~uint64_t(1);
+  m += (m & 1);
+  m >>= 1;
+  if (m >= (uint64_t(2) << 52)) {
+    m = uint64_t(1) << 52;
+    ++p2;
+  }
+  m &= ~(uint64_t(1) << 52);
+  if (p2 >= 0x7FF) return bits(0, 0x7FF);
+  return bits(m, p2);
+}
+
+const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                           1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+struct Scanner {
+  const char* p;
+  const char* end;
+
+  void ws() {
+    while (p < end && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+  bool eat(char c) {
+    if (p < end && *p == c) {
+      ++p;
+      return true;
+    }
+    return false;
+  }
+  bool lit(const char* s, size_t n) {
+    if (static_cast<size_t>(end - p) >= n && std::memcmp(p, s, n) == 0) {
+      p += n;
+      return true;
+    }
+    return false;
+  }
+  static bool digit(char c) { return c >= '0' && c <= '9'; }
+
+  static uint64_t load8(const char* q) {
+    uint64_t v;
+    std::memcpy(&v, q, 8);
+    return v;
+  }
+  // Number of leading ASCII digits in the 8 bytes of v (0..8).
+  static int digit_run(uint64_t v) {
+    const uint64_t x = v ^ 0x3030303030303030ULL;   // digits -> 0..9
+    const uint64_t bad = ((x + 0x7676767676767676ULL) | x) & 0x8080808080808080ULL;
+    return bad ? (__builtin_ctzll(bad) >> 3) : 8;
+  }
+  static uint32_t parse_eight(uint64_t v) {   // SWAR: 8 ASCII digits -> value
+    v = (v & 0x0F0F0F0F0F0F0F0FULL) * 2561 >> 8;
+    v = (v & 0x00FF00FF00FF00FFULL) * 6553601 >> 16;
+    return static_cast<uint32_t>((v & 0x0000FFFF0000FFFFULL) * 42949672960001ULL >> 32);
+  }
+  // The first n (1..7) digits of v as a number: shift them to the top and
+  // pad the low bytes with '0' (little endian: byte 0 is the first char).
+  static uint32_t parse_head(uint64_t v, int n) {
+    const int sh = (8 - n) * 8;
+    return parse_eight((v << sh) | (0x3030303030303030ULL >> (64 - sh)));
+  }
+
+  static constexpr uint64_t kP10[9] = {1, 10, 100, 1000, 10000, 100000, 1000000, 10000000,
+                                       100000000};
+
+  // Scan a run of digits at p into w.  Returns the run length; sets *ok =
+  // false if the run would push w past 19 digits (nd counts digits in w).
+  size_t digits(uint64_t& w, int& nd, bool* ok) {
+    const char* q = p;
+    if (end - p >= 16) {   // fast path: whole words readable
+      for (;;) {
+        const uint64_t v = load8(p);
+        const int n = digit_run(v);
+        if (n == 0) break;
+        if (nd + n > 19) {
+          *ok = false;
+          while (p < end && digit(*p)) ++p;
+          return static_cast<size_t>(p - q);
+        }
+        w = w * kP10[n] + (n == 8 ? parse_eight(v) : parse_head(v, n));
+        nd += n;
+        p += n;
+        if (n < 8 || end - p < 8) break;
+      }
+    }
+    while (p < end && digit(*p)) {
+      if (nd >= 19) {
+        *ok = false;
+        while (p < end && digit(*p)) ++p;
+        break;
+      }
+      w = w * 10 + static_cast<uint64_t>(*p - '0');
+      ++nd;
+      ++p;
+    }
+    return static_cast<size_t>(p - q);
+  }
+
+  // One JSON number (Python json's NUMBER_RE) or NaN / Infinity / -Infinity.
+  bool number(double* v) {
+    const char* s = p;
+    if (p >= end) return false;
+    const char c0 = *p;
+    if (c0 == 'N') {
+      if (!lit("NaN", 3)) return false;
+      *v = std::nan("");
+      return true;
+    }
+    if (c0 == 'I') {
+      if (!lit("Infinity", 8)) return false;
+      *v = HUGE_VAL;
+      return true;
+    }
+    bool neg = false;
+    if (c0 == '-') {
+      if (end - p > 1 && p[1] == 'I') {
+        if (!lit("-Infinity", 9)) return false;
+        *v = -HUGE_VAL;
+        return true;
+      }
+      neg = true;
+      ++p;
+    }
+    if (p >= end || !digit(*p)) return false;
+    uint64_t w = 0;
+    int nd = 0;
+    bool fits = true;                   // every significant digit is in w
+    size_t int_digits;
+    if (*p == '0') {
+      ++p;
+      int_digits = 1;
+    } else {
+      int_digits = digits(w, nd, &fits);
+    }
+    int frac = 0;
+    bool is_float = false;
+    if (p < end && *p == '.') {
+      ++p;
+      is_float = true;
+      const int nd0 = nd;
+      if (digits(w, nd, &fits) == 0) return false;
+      frac = nd - nd0;
+    }
+    long e10 = 0;
+    if (p < end && (*p == 'e' || *p == 'E')) {
+      ++p;
+      is_float = true;
+      bool eneg = false;
+      if (p < end && (*p == '+' || *p == '-')) eneg = *p++ == '-';
+      if (p >= end || !digit(*p)) return false;
+      while (p < end && digit(*p)) {
+        if (e10 < 100000) e10 = e10 * 10 + (*p - '0');
+        ++p;
+      }
+      if (eneg) e10 = -e10;
+    }
+    if (!is_float && int_digits > 18) return false;   // huge int literal: leave to Python
+    if (!is_float && w == 0) {   // Python ints have no -0: int("-0") -> 0 -> +0.0
+      *v = 0.0;
+      return true;
+    }
+    const bool exact = fits;
+    const long pw = e10 - frac;
+    if (exact && w <= (uint64_t(1) << 53) && pw >= -22 && pw <= 22) {
+      double d = static_cast<double>(w);
+      d = pw >= 0 ? d * kPow10[pw] : d / kPow10[-pw];
+      *v = neg ? -d : d;
+      return true;
+    }
+    if (exact) {   // every digit is in w (<= 19 of them)
+      *v = eisel_lemire(w, pw, neg);
+      return true;
+    }
+    // more than 19 significant digits: correctly rounded strtod
+    char small[128];
+    const size_t n = static_cast<size_t>(p - s);
+    std::string big;
+    const char* txt;
+    if (n < sizeof(small)) {
+      std::memcpy(small, s, n);
+      small[n] = 0;
+      txt = small;
+    } else {
+      big.assign(s, n);
+      txt = big.c_str();
+    }
+    char* q = nullptr;
+    *v = std::strtod(txt, &q);
+    return q == txt + n;
+  }
+};
+
+}  // namespace
+
+extern "C" int kf_parse_instances(const char* body, int64_t len, double* out, int64_t cap,
+                                  int64_t* rows, int64_t* cols) {
+  if (!body || len < 0 || !rows || !cols) return KF_FALLBACK;
+  *rows = 0;
+  *cols = 0;
+  Scanner sc{body, body + len};
+  sc.ws();
+  if (!sc.eat('{')) return KF_FALLBACK;
+  sc.ws();
+  if (!sc.lit("\"instances\"", 11)) return KF_FALLBACK;
+  sc.ws();
+  if (!sc.eat(':')) return KF_FALLBACK;
+  sc.ws();
+  if (!sc.eat('[')) return KF_FALLBACK;
+  int64_t r = 0, c = -1, n = 0;
+  bool overflow = false;
+  sc.ws();
+  if (sc.p < sc.end && *sc.p == ']') return KF_FALLBACK;   // empty instances: the error path
+  for (;;) {
+    sc.ws();
+    if (!sc.eat('[')) return KF_FALLBACK;
+    int64_t k = 0;
+    sc.ws();
+    if (sc.p < sc.end && *sc.p == ']') return KF_FALLBACK;   // empty row
+    for (;;) {
+      sc.ws();
+      double v;
+      if (!sc.number(&v)) return KF_FALLBACK;
+      if (n < cap) out[n] = v;
+      else overflow = true;
+      ++n;
+      ++k;
+      sc.ws();
+      if (sc.eat(',')) continue;
+      if (sc.eat(']')) break;
+      return KF_FALLBACK;
+    }
+    if (c < 0) c = k;
+    else if (k != c) return KF_FALLBACK;                     // ragged rows
+    ++r;
+    sc.ws();
+    if (sc.eat(',')) continue;
+    if (sc.eat(']')) break;
+    return KF_FALLBACK;
+  }
+  sc.ws();
+  if (!sc.eat('}')) return KF_FALLBACK;
+  sc.ws();
+  if (sc.p != sc.end) return KF_FALLBACK;
+  *rows = r;
+  *cols = c;
+  return overflow ? KF_ERR_SPACE : KF_PARSED;
+}

@@ -35,7 +35,9 @@ from concurrent.futures import ThreadPoolExecutor
 from http import HTTPStatus
 from typing import Dict, List, Optional, Tuple
 
+from . import fastjson
 from .errors import HTTPError
+from .kfmodel import KFModel
 from .kfmodel_repository import KFModelRepository
 
 DEFAULT_HTTP_PORT = 8080
@@ -55,6 +57,8 @@ parser.add_argument('--max_batchsize', default=0, type=int,
                     help='Enable the in-process batcher with this many rows per batch (0 = off).')
 parser.add_argument('--max_latency_ms', default=5000, type=int,
                     help='Batcher flush latency in milliseconds.')
+parser.add_argument('--no_fast_json', action='store_true',
+                    help='Decode every body with json.loads (no native v1 parser).')
 args, _ = parser.parse_known_args()
 
 JSON_CT = "application/json; charset=UTF-8"
@@ -95,8 +99,14 @@ class Application:
     """Route table + handlers, independent of the socket transport."""
 
     def __init__(self, models: KFModelRepository, executor: Optional[ThreadPoolExecutor] = None,
-                 batcher_factory=None):
+                 batcher_factory=None, fast_json: bool = True):
         self.models = models
+        # native v1 body decode (libkfserve.so) for models that take the
+        # decoded matrix (accepts_array_instances); loaded here so a missing
+        # library fails at start-up, not on the first request
+        self.fast_json = fast_json
+        if fast_json:
+            fastjson.load_library()
         self.executor = executor or ThreadPoolExecutor(max_workers=8)
         self._batchers = {}
         self._batcher_factory = batcher_factory
@@ -162,7 +172,9 @@ class Application:
     @staticmethod
     def validate(request):
         if isinstance(request, dict):
-            if ("instances" in request and not isinstance(request["instances"], list)) or \
+            inst = request.get("instances")
+            if ("instances" in request and not isinstance(inst, list)
+                    and not isinstance(inst, fastjson.JsonInstances)) or \
                ("inputs" in request and not isinstance(request["inputs"], list)):
                 raise HTTPError(HTTPStatus.BAD_REQUEST,
                                 "Expected \"instances\" or \"inputs\" to be a list")
@@ -174,11 +186,21 @@ class Application:
         return await asyncio.get_running_loop().run_in_executor(self.executor, fn, request)
 
     async def predict(self, headers, body, name):
-        try:
-            request = json.loads(body)
-        except (json.JSONDecodeError, UnicodeDecodeError) as e:
-            raise HTTPError(HTTPStatus.BAD_REQUEST, "Unrecognized request format: %s" % e)
+        X = fastjson.parse_instances(body) if self.fast_json else None
+        if X is None:
+            try:
+                request = json.loads(body)
+            except (json.JSONDecodeError, UnicodeDecodeError) as e:
+                raise HTTPError(HTTPStatus.BAD_REQUEST, "Unrecognized request format: %s" % e)
         model = self.get_model(name)
+        if X is not None:
+            # the decoded matrix goes only to models that take it and keep the
+            # base preprocess (identity for this body shape); others get lists
+            if getattr(model, "accepts_array_instances", False) and \
+                    type(model).preprocess is KFModel.preprocess:
+                request = {"instances": X}
+            else:
+                request = json.loads(body)
         request = model.preprocess(request)
         request = self.validate(request)
         if self._batcher_factory is not None and isinstance(request, dict) \
@@ -289,7 +311,8 @@ class KFServer:
                  workers: int = args.workers,
                  registered_models: KFModelRepository = None,
                  max_batchsize: int = args.max_batchsize,
-                 max_latency_ms: int = args.max_latency_ms):
+                 max_latency_ms: int = args.max_latency_ms,
+                 fast_json: bool = not args.no_fast_json):
         self.registered_models = registered_models if registered_models is not None \
             else KFModelRepository()
         self.http_port = http_port
@@ -298,6 +321,7 @@ class KFServer:
         self.workers = workers
         self.max_batchsize = max_batchsize
         self.max_latency_ms = max_latency_ms
+        self.fast_json = fast_json
         self._server = None
         self._sock: Optional[socket.socket] = None
 
@@ -309,7 +333,8 @@ class KFServer:
 
             def factory(model, call):
                 return ModelBatcher(model, call, max_batch_size=size, max_latency_ms=lat)
-        return Application(self.registered_models, batcher_factory=factory)
+        return Application(self.registered_models, batcher_factory=factory,
+                           fast_json=self.fast_json)
 
     def register_model(self, model) -> None:
         if not model.name:

@@ -19,6 +19,9 @@ from .forest import OUT_PREDICT, Forest
 
 
 class GPUForestMixin:
+    # KFServer may hand predict() the natively decoded float64 matrix
+    # (kfserving.fastjson.JsonInstances) instead of a list of lists
+    accepts_array_instances = True
     _forest: Optional[Forest] = None
     _device_forest: Optional[DeviceForest] = None
     devices: Optional[Sequence[int]] = None

@@ -12,6 +12,7 @@ import numpy as np
 
 from ..formats.xgboost_format import load_xgboost_model
 from ..forest import Forest
+from ..kfserving.fastjson import JsonInstances
 from ..kfserving.kfmodel import KFModel
 from ..kfserving.storage import Storage
 from ..tree_model import GPUForestMixin, xgb_matrix_from_list
@@ -38,10 +39,10 @@ class XGBoostModel(GPUForestMixin, KFModel):
     def predict(self, request: Dict) -> Dict:
         try:
             instances = request["instances"]
-            if isinstance(instances, np.ndarray):
+            if isinstance(instances, np.ndarray) and not isinstance(instances, JsonInstances):
                 X = instances                      # DMatrix(ndarray): NaN = missing
             else:
-                X = xgb_matrix_from_list(instances)   # DMatrix(list) semantics
+                X = xgb_matrix_from_list(instances)   # DMatrix(list) semantics (JSON rows)
             result = self.predict_matrix(X)
             return {"predictions": result.tolist()}
         except Exception as e:

@@ -76,3 +76,13 @@ def test_abi_constants_match_python():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(engine.TreeInferError):
         engine.load_library(str(tmp_path / "nope.so"))
+
+
+def test_kfserve_library_exports_its_header():
+    from kfserving_amd.kfserving import fastjson
+    src = open(os.path.join(ROOT, "include", "kfserve.h")).read()
+    names = sorted(set(re.findall(r"^\s*int\s+(kf_\w+)\(", src, re.M)))
+    assert names == ["kf_parse_instances"]
+    lib = fastjson.load_library()
+    for n in names:
+        assert hasattr(lib, n), n

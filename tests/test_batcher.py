@@ -167,3 +167,31 @@ def test_bench_batched_latency_leg_on_cpu():
     assert r["requests"] == 1000 and r["batches"] >= 1
     assert 1.0 <= r["p50_ms"] < 100 and r["p99_ms"] >= r["p50_ms"]
     assert r["mean_batch_rows"] > 32
+
+
+def test_matrix_chunks_concatenate_and_fan_out():
+    import numpy as np
+    from kfserving_amd.kfserving.fastjson import JsonInstances
+    seen = []
+
+    async def predict_batch(instances):
+        seen.append(instances)
+        X = np.asarray(instances, dtype=np.float64)
+        return {"predictions": X.sum(axis=1).tolist()}
+
+    async def go():
+        b = Batcher(predict_batch, max_batch_size=6, max_latency_ms=1000)
+        m1 = np.array([[1.0, 2.0], [3.0, 4.0]]).view(JsonInstances)
+        m2 = np.array([[5.0, 6.0]]).view(JsonInstances)
+        m3 = np.array([[7.0, 8.0], [9.0, 10.0], [11.0, 12.0]]).view(JsonInstances)
+        r = await asyncio.gather(b.submit(m1), b.submit(m2), b.submit(m3))
+        mixed = await asyncio.gather(b.submit([[1, 1]]), b.submit(m2), b.submit([[2, 2]] * 4))
+        return r, mixed
+    r, mixed = run(go())
+    assert isinstance(seen[0], JsonInstances) and seen[0].shape == (6, 2)
+    assert [x["predictions"] for x in r] == [[3.0, 7.0], [11.0], [15.0, 19.0, 23.0]]
+    assert len({x["batchId"] for x in r}) == 1
+    assert isinstance(seen[1], list) and len(seen[1]) == 6          # mixed -> rows list
+    assert [x["predictions"] for x in mixed] == [[2.0], [11.0], [4.0] * 4]
+    with pytest.raises(Exception):
+        run(Batcher(predict_batch).submit(np.zeros((0, 3))))

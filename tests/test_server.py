@@ -204,3 +204,76 @@ def test_in_process_batcher_route(serve):
 def test_httperror_reason():
     e = HTTPError(404, "x")
     assert e.status_code == 404 and e.reason == "x"
+
+
+# ------------------------------------------------ native body decode (fast path)
+class ArrayModel(KFModel):
+    """Takes the natively decoded matrix, like the tree plugins; predicts a
+    row checksum through the DMatrix(list) conversion (0 -> missing)."""
+    accepts_array_instances = True
+
+    def __init__(self, name):
+        super().__init__(name)
+        self.ready = True
+        self.seen = []
+
+    def predict(self, request):
+        import numpy as np
+        from kfserving_amd.tree_model import xgb_matrix_from_list
+        inst = request["instances"]
+        self.seen.append(type(inst).__name__)
+        X = xgb_matrix_from_list(inst)
+        return {"predictions": np.nan_to_num(X, nan=-7.0).sum(axis=1).tolist()}
+
+
+class CustomPre(ArrayModel):
+    def preprocess(self, request):
+        assert isinstance(request["instances"], list)
+        return request
+
+
+FAST_BODIES = [
+    b'{"instances": [[1, 2.5, 0, -0.0], [3, 4, 5e-3, NaN]]}',
+    b'{ "instances" : [ [0.1,0.2 ,0.30000000000000004,1e22] ] }',
+    b'{"instances": [[Infinity, -Infinity, 7, 123456789012345678]]}',
+    b'{"instances": [[1, 2], [3]]}',                 # ragged: json.loads path
+    b'{"instances": [[1, 2]], "signature_name": "x"}',
+    b'{"instances": []}',
+    b'{"instances": [[1, 2]',                        # malformed: 400 either way
+]
+
+
+@pytest.mark.parametrize("batch", [0, 4])
+def test_fast_json_bytes_match_json_loads_path(serve, batch):
+    outs = {}
+    for fast in (True, False):
+        server = KFServer(registered_models=KFModelRepository(), fast_json=fast,
+                          max_batchsize=batch, max_latency_ms=5)
+        model = ArrayModel("m")
+        server.register_model(model)
+        s = serve(server)
+        outs[fast] = [s.fetch("/v1/models/m:predict", "POST", b) for b in FAST_BODIES]
+        if fast:
+            assert "JsonInstances" in model.seen
+        else:
+            assert "JsonInstances" not in model.seen
+    for (c1, h1, b1), (c2, h2, b2) in zip(outs[True], outs[False]):
+        if batch and c1 == 200:   # batchId is random
+            b1, b2 = json.loads(b1), json.loads(b2)
+            if isinstance(b1, dict):
+                b1.pop("batchId", None)
+                b2.pop("batchId", None)
+        assert (c1, b1) == (c2, b2)
+        assert h1["Content-Type"] == h2["Content-Type"]
+
+
+def test_fast_json_not_for_custom_preprocess_or_plain_models(serve):
+    server = KFServer(registered_models=KFModelRepository())
+    m1, m2 = CustomPre("c"), SyncModel("s")
+    server.register_model(m1)
+    server.register_model(m2)
+    s = serve(server)
+    code, _, body = s.fetch("/v1/models/c:predict", "POST", b'{"instances": [[1, 2]]}')
+    assert code == 200 and m1.seen == ["list"]
+    code, _, body = s.fetch("/v1/models/s:predict", "POST", b'{"instances": [[1, 2]]}')
+    assert code == 200 and json.loads(body) == {"predictions": [[2, 4]]}
