@@ -90,6 +90,37 @@ def tune_gc() -> None:
     gc.set_threshold(50_000, 50, 100)
 
 
+def gpu_count_without_init() -> int:
+    """GPUs the KFD driver exposes, counted from sysfs (no HIP call: the
+    workers fork after this and must initialise HIP themselves)."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "gpu_id")) as fh:
+                    n += int(fh.read().strip() or 0) != 0
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        return 0
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    if vis:
+        n = min(n, len([v for v in vis.split(",") if v.strip()]))
+    return n
+
+
+def pin_worker_device(index: int, workers: int) -> None:
+    """With several pre-forked workers and several GPUs, worker i drives GPU
+    i mod n (its forest replica lives there) unless TREEINFER_DEVICES says
+    otherwise; a single worker keeps every GPU and row-shards each batch."""
+    if workers <= 1 or os.environ.get("TREEINFER_DEVICES"):
+        return
+    n = gpu_count_without_init()
+    if n > 1:
+        os.environ["TREEINFER_DEVICES"] = str(index % n)
+
+
 def error_response(code: int, reason: str) -> Response:
     page = "<html><title>%d: %s</title><body>%d: %s</body></html>" % (code, reason, code, reason)
     return code, reason, {"Content-Type": HTML_CT}, page.encode("utf-8")
@@ -376,7 +407,7 @@ class KFServer:
         sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         sock.bind((host, self.http_port))
-        sock.listen(1024)
+        sock.listen(4096)
         sock.setblocking(False)
         self.http_port = sock.getsockname()[1]
         self._sock = sock
@@ -398,7 +429,10 @@ class KFServer:
         tune_gc()
         logging.info("Listening on port %s", self.http_port)
         logging.info("Will fork %d workers", self.workers)
-        for _ in range(max(0, self.workers - 1)):
+        index = 0
+        for i in range(1, max(1, self.workers)):
             if os.fork() == 0:    # child: serve on the shared socket (GPU is lazily initialised)
+                index = i
                 break
+        pin_worker_device(index, self.workers)
         asyncio.run(self.serve(sock))

@@ -1,0 +1,162 @@
+"""C5 serving benchmark: many concurrent HTTP clients of
+1-64-row v1 :predict requests, open-loop at fixed aggregate QPS, through
+KFServer's in-process batcher (maxBatchSize 65,536 rows, maxLatency 5 ms)
+into the GPU engine.  Model: the C2 forest (500 depth-8 trees, 28 features,
+XGBoost legacy binary, binary:logistic).
+
+  python scripts/bench_serving.py [--qps 5000,10000,20000] [--conns 4096]
+        [--workers 4] [--duration 10] [--model c2|dummy]
+
+Starts `python -m kfserving_amd.xgbserver` as a child process (its own
+process group, ended by PID), drives it with the C load generator
+(kfserving_amd/lib/loadgen, built by __graft_entry__.build), prints one JSON
+line per QPS point.  --model dummy serves a CPU echo model (no GPU) for
+testing the harness itself.
+"""
+import argparse
+import http.client
+import json
+import os
+import resource
+import signal
+import struct
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+LOADGEN = os.path.join(ROOT, "kfserving_amd", "lib", "loadgen")
+
+DUMMY_SERVER = r'''
+import sys
+sys.path.insert(0, %(root)r)
+from kfserving_amd.kfserving import KFModel, KFServer, KFModelRepository
+class Echo(KFModel):
+    accepts_array_instances = True
+    def __init__(self):
+        super().__init__("model"); self.ready = True
+    def predict(self, request):
+        return {"predictions": [0.5] * len(request["instances"])}
+KFServer(http_port=%(port)d, workers=%(workers)d, max_batchsize=%(mbs)d,
+         max_latency_ms=%(lat)d, registered_models=KFModelRepository()).start([Echo()])
+'''
+
+
+def write_bodies(path, n_feat, variants, seed):
+    rng = np.random.default_rng(seed)
+    with open(path, "wb") as fh:
+        fh.write(struct.pack("<I", variants))
+        for r in range(1, 65):
+            for _ in range(variants):
+                X = rng.standard_normal((r, n_feat), dtype=np.float32)
+                b = json.dumps({"instances": X.tolist()}).encode()
+                fh.write(struct.pack("<I", len(b)))
+                fh.write(b)
+
+
+def write_c2_model(d):
+    from kfserving_amd.formats.xgboost_format import (synthetic_complete_trees,
+                                                      write_legacy_binary)
+    trees, ti = synthetic_complete_trees(500, 8, 28, seed=0)
+    write_legacy_binary(os.path.join(d, "model.bst"), trees, ti, 28, 0, 0.5,
+                        "binary:logistic")
+
+
+def wait_ready(port, timeout=180):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=2)
+            c.request("GET", "/v1/models/model")
+            r = c.getresponse()
+            r.read()
+            c.close()
+            if r.status == 200:
+                return True
+        except OSError:
+            pass
+        time.sleep(0.5)
+    return False
+
+
+def warm(port, n_feat, n=20):
+    body = json.dumps({"instances": np.zeros((64, n_feat)).tolist()}).encode()
+    for _ in range(n):
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+        c.request("POST", "/v1/models/model:predict", body=body,
+                  headers={"Content-Type": "application/json"})
+        r = c.getresponse()
+        r.read()
+        c.close()
+        if r.status != 200:
+            raise RuntimeError(f"warm-up predict returned {r.status}")
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--qps", default="5000,10000,20000")
+    p.add_argument("--conns", type=int, default=4096)
+    p.add_argument("--workers", type=int, default=4)
+    p.add_argument("--duration", type=float, default=8.0)
+    p.add_argument("--warmup", type=float, default=2.0)
+    p.add_argument("--port", type=int, default=18080)
+    p.add_argument("--model", default="c2", choices=["c2", "dummy"])
+    p.add_argument("--max-batch", type=int, default=65536)
+    p.add_argument("--max-latency-ms", type=int, default=5)
+    args = p.parse_args()
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    resource.setrlimit(resource.RLIMIT_NOFILE, (hard, hard))
+    n_feat = 28
+    tmp = tempfile.mkdtemp()
+    bodies = os.path.join(tmp, "bodies.bin")
+    write_bodies(bodies, n_feat, 8, seed=3)
+    env = dict(os.environ)
+    if args.model == "c2":
+        write_c2_model(tmp)
+        cmd = [sys.executable, "-m", "kfserving_amd.xgbserver", "--model_dir", tmp,
+               "--model_name", "model", "--http_port", str(args.port),
+               "--workers", str(args.workers), "--max_batchsize", str(args.max_batch),
+               "--max_latency_ms", str(args.max_latency_ms)]
+    else:
+        code = DUMMY_SERVER % {"root": ROOT, "port": args.port, "workers": args.workers,
+                               "mbs": args.max_batch, "lat": args.max_latency_ms}
+        cmd = [sys.executable, "-c", code]
+    server = subprocess.Popen(cmd, cwd=ROOT, env=env, start_new_session=True,
+                              stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "server.log"), "w"))
+    try:
+        if not wait_ready(args.port):
+            raise RuntimeError("server did not become ready: " +
+                               open(os.path.join(tmp, "server.log")).read()[-2000:])
+        warm(args.port, n_feat)
+        for q in [float(x) for x in args.qps.split(",")]:
+            out = subprocess.run([LOADGEN, "--port", str(args.port), "--conns", str(args.conns),
+                                  "--qps", str(q), "--duration", str(args.duration),
+                                  "--warmup", str(args.warmup), "--bodies", bodies,
+                                  "--path", "/v1/models/model:predict"],
+                                 capture_output=True, text=True, timeout=args.duration * 3 + 120)
+            if out.returncode != 0:
+                raise RuntimeError(f"loadgen failed: {out.stderr[-2000:]}")
+            res = json.loads(out.stdout)
+            res.update({"config": "C5 dynamic batching: v1 :predict over HTTP, KFServer "
+                                  "in-process batcher", "model": args.model,
+                        "workers": args.workers, "max_batch_size": args.max_batch,
+                        "max_latency_ms": args.max_latency_ms,
+                        "gpus_visible": os.environ.get("TREEINFER_DEVICES", "all")})
+            print(json.dumps(res), flush=True)
+    finally:
+        try:
+            os.killpg(server.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+        try:
+            server.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            os.killpg(server.pid, signal.SIGKILL)
+
+
+if __name__ == "__main__":
+    main()
