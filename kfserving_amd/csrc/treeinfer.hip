@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cmath>
+#include <limits>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -121,6 +122,9 @@ struct DeviceForest {
   // binned heap layout: one image + threshold tables per input dtype
   unsigned char* bh_img[2] = {nullptr, nullptr};
   unsigned char* bh_tbl[2] = {nullptr, nullptr};
+  // binned explicit layout: rank-coded nodes + tables per input dtype
+  ExpNode* bx_nodes[2] = {nullptr, nullptr};
+  unsigned char* bx_tbl[2] = {nullptr, nullptr};
   // ti_predict scratch: device buffers + pinned host staging (grown x2)
   void* x_buf = nullptr;
   size_t x_cap = 0;
@@ -166,6 +170,16 @@ struct ti_forest {
     int32_t words = 0;                // packed bin words per row
     int64_t stride = 0;
   } bh[2];
+  // binned explicit layout (4): explicit nodes whose threshold is a rank
+  struct BinExplicit {
+    std::vector<ExpNode> nodes;
+    std::vector<unsigned char> tbl;
+    int32_t L = 0;
+    int32_t b16 = 1;
+    int32_t rows = 256;
+    int32_t words = 0;
+  } bx[2];
+  std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
   // host images (kept until upload)
   std::vector<unsigned char> h_heap32, h_heap64;
   std::vector<int32_t> h_heap_leaf_ids;
@@ -199,7 +213,8 @@ void free_device(DeviceForest& d) {
                   d.leaf_base, d.leaves, d.exp_leaf_ids, d.tree_group, d.x_buf, d.out_buf,
                   d.cpt_img[0], d.cpt_img[1], d.cpt_off[0], d.cpt_off[1], d.cpt_stage[0],
                   d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root, d.cat_words,
-                  d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1]};
+                  d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1],
+                  d.bx_nodes[0], d.bx_nodes[1], d.bx_tbl[0], d.bx_tbl[1]};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d.hx_pin) (void)hipHostFree(d.hx_pin);
@@ -220,7 +235,10 @@ void free_device(DeviceForest& d) {
   }
   d.cpt_nint = d.cpt_depth = d.cpt_root = nullptr;
   d.cat_words = nullptr;
-  for (int i = 0; i < 2; ++i) d.bh_img[i] = d.bh_tbl[i] = nullptr;
+  for (int i = 0; i < 2; ++i) {
+    d.bh_img[i] = d.bh_tbl[i] = d.bx_tbl[i] = nullptr;
+    d.bx_nodes[i] = nullptr;
+  }
   d.x_cap = d.out_cap = 0;
   d.stream = nullptr;
   d.device = -1;
@@ -350,6 +368,7 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
   const int LW = d->leaf_width;
   f->h_nodes.clear();
   f->h_thr64.clear();
+  f->h_exp_src.clear();
   f->h_node_base.assign(d->n_trees, 0);
   f->h_leaf_base.assign(d->n_trees, 0);
   f->h_root.assign(d->n_trees, 0);
@@ -385,6 +404,7 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
     }
     f->h_nodes.resize(nb + n_int);
     f->h_thr64.resize(nb + n_int);
+    f->h_exp_src.resize(nb + n_int);
     for (size_t qi = 0; qi < queue.size(); ++qi) {
       const int32_t v = queue[qi];
       const int64_t g = b + v;
@@ -405,6 +425,7 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
       e.right = remap[d->right[g]];
       f->h_nodes[nb + remap[v]] = e;
       f->h_thr64[nb + remap[v]] = d->threshold[g];
+      f->h_exp_src[nb + remap[v]] = g;
     }
     f->h_root[t] = remap[0];
   }
@@ -549,23 +570,76 @@ void eytzinger_fill(const std::vector<double>& sorted, std::vector<double>* out,
   eytzinger_fill(sorted, out, 2 * k + 1, i);
 }
 
+// Per-feature rank tables of one XT view.  With zero_bins, every feature
+// that a LightGBM zero-missing node tests also gets the thresholds {-denorm_min,
+// 0}: then exactly x == 0 (+-0) falls in the bin 1 + index(0) (zbin), so the
+// zero rule becomes an integer compare as well.
+template <typename XT>
+struct RankTables {
+  std::vector<std::vector<XT>> u;   // sorted distinct thresholds per feature
+  std::vector<uint32_t> zbin;       // bin of exact 0 per feature (0: none)
+  size_t m_max = 0;
+  int L = 0;
+
+  uint32_t rank(int f, double thr) const {
+    const XT t = threshold_view<XT>(thr);
+    if (std::isnan(static_cast<double>(t))) return 0;   // NaN threshold: never left
+    return 1u + static_cast<uint32_t>(std::lower_bound(u[f].begin(), u[f].end(), t) - u[f].begin());
+  }
+};
+
+template <typename XT>
+RankTables<XT> collect_ranks(const ti_forest_desc* d, bool zero_bins) {
+  RankTables<XT> rt;
+  const int F = d->n_features;
+  rt.u.assign(F, {});
+  rt.zbin.assign(F, 0);
+  std::vector<char> zf(F, 0);
+  for (int64_t g = 0; g < d->n_nodes; ++g) {
+    if (d->feature[g] < 0 || (d->flags[g] & TI_NODE_CATEGORICAL)) continue;
+    const XT t = threshold_view<XT>(d->threshold[g]);
+    if (!std::isnan(static_cast<double>(t))) rt.u[d->feature[g]].push_back(t);
+    if (zero_bins && (d->flags[g] & TI_NODE_ZERO_FLIP)) zf[d->feature[g]] = 1;
+  }
+  for (int f = 0; f < F; ++f) {
+    auto& v = rt.u[f];
+    if (zf[f]) {
+      v.push_back(XT(0));
+      v.push_back(-std::numeric_limits<XT>::denorm_min());
+    }
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    rt.m_max = std::max(rt.m_max, v.size());
+    if (zf[f]) rt.zbin[f] = 1u + static_cast<uint32_t>(std::lower_bound(v.begin(), v.end(), XT(0)) - v.begin());
+  }
+  while ((static_cast<size_t>(1) << rt.L) - 1 < rt.m_max) ++rt.L;
+  return rt;
+}
+
+// [F][2^L] Eytzinger search tables (1-based, +inf padded) as XT bytes.
+template <typename XT>
+void eytzinger_tables(const RankTables<XT>& rt, std::vector<unsigned char>* out) {
+  const int F = static_cast<int>(rt.u.size());
+  const size_t tsz = static_cast<size_t>(1) << rt.L;
+  out->assign(static_cast<size_t>(F) * tsz * sizeof(XT), 0);
+  XT* tbl = reinterpret_cast<XT*>(out->data());
+  std::vector<double> srt, ey(tsz);
+  for (int f = 0; f < F; ++f) {
+    srt.assign(rt.u[f].begin(), rt.u[f].end());
+    size_t i = 0;
+    std::fill(ey.begin(), ey.end(), static_cast<double>(INFINITY));
+    eytzinger_fill(srt, &ey, 1, &i);
+    for (size_t k = 0; k < tsz; ++k) tbl[f * tsz + k] = static_cast<XT>(ey[k]);
+  }
+}
+
 template <typename XT, typename ACC>
 bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
                 std::vector<int32_t>* leaf_ids) {
   const int F = d->n_features;
   const int LW = d->leaf_width;
-  std::vector<std::vector<XT>> u(F);
-  for (int64_t g = 0; g < d->n_nodes; ++g) {
-    if (d->feature[g] < 0 || (d->flags[g] & TI_NODE_CATEGORICAL)) continue;
-    const XT t = threshold_view<XT>(d->threshold[g]);
-    if (!std::isnan(static_cast<double>(t))) u[d->feature[g]].push_back(t);
-  }
-  size_t m_max = 0;
-  for (auto& v : u) {
-    std::sort(v.begin(), v.end());
-    v.erase(std::unique(v.begin(), v.end()), v.end());
-    m_max = std::max(m_max, v.size());
-  }
+  const RankTables<XT> rt = collect_ranks<XT>(d, false);
+  const size_t m_max = rt.m_max;
   if (m_max > 65533) return false;
   bi->b16 = m_max > 253 ? 1 : 0;
   const int P = bi->b16 ? 2 : 4;
@@ -575,26 +649,11 @@ bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
     R >>= 1;
   if (static_cast<int64_t>(bi->words) * R * 4 > static_cast<int64_t>(ti::kBNodeOffMask) + 1) return false;
   bi->rows = R;
-  int L = 0;
-  while ((static_cast<size_t>(1) << L) - 1 < m_max) ++L;
-  bi->L = L;
-  const size_t tsz = static_cast<size_t>(1) << L;
-  bi->tbl.assign(static_cast<size_t>(F) * tsz * sizeof(XT), 0);
-  XT* tbl = reinterpret_cast<XT*>(bi->tbl.data());
-  std::vector<double> srt, ey(tsz);
-  for (int f = 0; f < F; ++f) {
-    srt.assign(u[f].begin(), u[f].end());
-    size_t i = 0;
-    std::fill(ey.begin(), ey.end(), static_cast<double>(INFINITY));
-    eytzinger_fill(srt, &ey, 1, &i);
-    for (size_t k = 0; k < tsz; ++k) tbl[f * tsz + k] = static_cast<XT>(ey[k]);
-  }
+  bi->L = rt.L;
+  eytzinger_tables(rt, &bi->tbl);
   auto node_word = [&](int64_t g) -> uint32_t {
     const int f = d->feature[g];
-    const XT t = threshold_view<XT>(d->threshold[g]);
-    uint32_t rank = 0;   // NaN threshold: never left
-    if (!std::isnan(static_cast<double>(t)))
-      rank = 1u + static_cast<uint32_t>(std::lower_bound(u[f].begin(), u[f].end(), t) - u[f].begin());
+    const uint32_t rank = rt.rank(f, d->threshold[g]);
     const uint32_t off = static_cast<uint32_t>((f / P) * R * 4 + (f % P) * (4 / P));
     uint32_t w = off | (rank << 16);
     if (d->flags[g] & TI_NODE_NAN_LEFT) w |= ti::kBNodeNanLeft;
@@ -637,6 +696,38 @@ bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
   return true;
 }
 
+// Rank-coded copy of the explicit nodes (pack_explicit must have run).
+// Returns false when a feature has more than 65,533 distinct thresholds or the
+// bin image does not fit 64 KB even at 64-row tiles.
+template <typename XT>
+bool pack_bexplicit(const ti_forest_desc* d, ti_forest* f, ti_forest::BinExplicit* bx) {
+  const RankTables<XT> rt = collect_ranks<XT>(d, f->zero_rule != 0);
+  if (rt.m_max > 65533) return false;
+  bx->b16 = rt.m_max > 253 ? 1 : 0;
+  const int P = bx->b16 ? 2 : 4;
+  bx->words = (d->n_features + P - 1) / P;
+  int R = env_int("TI_BEXP_ROWS", 256);
+  while (R > 64 && static_cast<size_t>(bx->words) * R * 4 > kFeatLdsMax) R >>= 1;
+  if (static_cast<size_t>(bx->words) * R * 4 > kFeatLdsMax) return false;
+  bx->rows = R;
+  bx->L = rt.L;
+  eytzinger_tables(rt, &bx->tbl);
+  bx->nodes.resize(f->h_nodes.size());
+  for (size_t i = 0; i < f->h_nodes.size(); ++i) {
+    const int64_t g = f->h_exp_src[i];
+    const int fe = d->feature[g];
+    ExpNode e = f->h_nodes[i];
+    const bool zflip = (d->flags[g] & TI_NODE_ZERO_FLIP) != 0;
+    const uint32_t w = rt.rank(fe, d->threshold[g]) | ((zflip ? rt.zbin[fe] : 0u) << 16);
+    std::memcpy(&e.thr, &w, sizeof(w));
+    e.meta = static_cast<uint32_t>((fe / P) * R * 4 + (fe % P) * (4 / P));
+    if (d->flags[g] & TI_NODE_NAN_LEFT) e.meta |= ti::kMetaNanLeft;
+    if (zflip) e.meta |= ti::kMetaZeroFlip;
+    bx->nodes[i] = e;
+  }
+  return true;
+}
+
 int upload_device(ti_forest* f, DeviceForest& d, int device) {
   d.device = device;
   TI_HIP(hipSetDevice(device));
@@ -647,6 +738,18 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
     if ((rc = upload(&d.heap32, f->h_heap32, &d.bytes))) return rc;
     if ((rc = upload(&d.heap64, f->h_heap64, &d.bytes))) return rc;
     if ((rc = upload(&d.heap_leaf_ids, f->h_heap_leaf_ids, &d.bytes))) return rc;
+  } else if (f->layout == 4) {
+    for (int i = 0; i < 2; ++i) {
+      if ((rc = upload(&d.bx_nodes[i], f->bx[i].nodes, &d.bytes))) return rc;
+      if ((rc = upload(&d.bx_tbl[i], f->bx[i].tbl, &d.bytes))) return rc;
+    }
+    if ((rc = upload(&d.node_base, f->h_node_base, &d.bytes))) return rc;
+    if ((rc = upload(&d.root, f->h_root, &d.bytes))) return rc;
+    if ((rc = upload(&d.leaf_base, f->h_leaf_base, &d.bytes))) return rc;
+    unsigned char* lv = nullptr;
+    if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
+    d.leaves = lv;
+    if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
   } else if (f->layout == 3) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.bh_img[i], f->bh[i].img, &d.bytes))) return rc;
@@ -698,6 +801,13 @@ KernelFn select_bheap(int xdt, int accum, int K, bool b16, int pf) {
   return ti::kernels_df(3, K, true, false, b16, pf);
 }
 
+KernelFn select_bexplicit(int xdt, int accum, int K, bool b16, bool z) {
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(4, K, true, z, b16, 0);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(4, K, true, z, b16, 0);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(4, K, true, z, b16, 0);
+  return ti::kernels_df(4, K, true, z, b16, 0);
+}
+
 std::mutex g_attr_mu;
 std::set<std::pair<int, const void*>> g_attr_done;
 
@@ -746,6 +856,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     R = ci.feat_lds ? ci.rows : 0;
   } else if (f->layout == 3) {
     R = f->bh[xdt == TI_F64 ? 1 : 0].rows;
+  } else if (f->layout == 4) {
+    R = f->bx[xdt == TI_F64 ? 1 : 0].rows;
   } else {
     R = 256;
     while (R > 64 && static_cast<size_t>(f->F) * R * xs > kFeatLdsMax) R >>= 1;
@@ -755,6 +867,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   if (!feat_lds) R = 256;
   size_t feat_bytes = feat_lds ? align16(static_cast<size_t>(f->F) * R * xs) : 0;
   if (f->layout == 3) feat_bytes = static_cast<size_t>(f->bh[xdt == TI_F64 ? 1 : 0].words) * R * 4;
+  if (f->layout == 4) feat_bytes = static_cast<size_t>(f->bx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
 
   KArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -847,6 +960,27 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
                                                         static_cast<size_t>(f->F + 7) & ~size_t(7)));
     lds = fixed + ar;
     KernelFn fn = select_bheap(xdt, f->accum, f->K, bi.b16 != 0, pf);
+    int rc = ensure_lds_attr(d.device, fn);
+    if (rc) return rc;
+    const int64_t grid = (rows + R - 1) / R;
+    if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    TI_HIP(hipGetLastError());
+    return TI_OK;
+  } else if (f->layout == 4) {
+    const int ii = xdt == TI_F64 ? 1 : 0;
+    const ti_forest::BinExplicit& bx = f->bx[ii];
+    a.nodes = d.bx_nodes[ii];
+    a.node_base = d.node_base;
+    a.root = d.root;
+    a.leaf_base = d.leaf_base;
+    a.leaves = d.leaves;
+    a.exp_leaf_ids = d.exp_leaf_ids;
+    a.bin_tbl = d.bx_tbl[ii];
+    a.bin_L = bx.L;
+    a.bin_words = bx.words;
+    lds = feat_bytes + 16;
+    KernelFn fn = select_bexplicit(xdt, f->accum, f->K, bx.b16 != 0, f->zero_rule != 0);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -999,7 +1133,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   bool use_compact = false;
   if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
   if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
-  if (want == "explicit") { use_heap = false; use_compact = false; }
+  if (want == "explicit" || want == "bexplicit") { use_heap = false; use_compact = false; }
   // categorical splits are evaluated by the explicit kernel only
   if (f->has_cat) { use_heap = false; use_compact = false; }
   if (use_compact) {
@@ -1062,6 +1196,16 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
       pack_explicit<double>(desc, f.get(), false);
     else
       pack_explicit<float>(desc, f.get(), false);
+    // rank-binned explicit nodes unless a categorical split needs raw values
+    // (TI_FORCE_LAYOUT=explicit keeps the float-compare kernel)
+    if (!f->has_cat && want != "explicit" && env_int("TI_NO_BEXPLICIT", 0) == 0) {
+      if (pack_bexplicit<float>(desc, f.get(), &f->bx[0]) &&
+          pack_bexplicit<double>(desc, f.get(), &f->bx[1])) {
+        f->layout = 4;
+      } else {
+        for (auto& bx : f->bx) bx = ti_forest::BinExplicit();
+      }
+    }
   }
   for (int i = 0; i < n_devices; ++i) {
     f->devs.emplace_back(new DeviceForest());
@@ -1083,6 +1227,14 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
     ci.img.clear();
     ci.img.shrink_to_fit();
   }
+  for (auto& bx : f->bx) {
+    bx.nodes.clear();
+    bx.nodes.shrink_to_fit();
+    bx.tbl.clear();
+    bx.tbl.shrink_to_fit();
+  }
+  f->h_exp_src.clear();
+  f->h_exp_src.shrink_to_fit();
   for (auto& bi : f->bh) {
     bi.img.clear();
     bi.img.shrink_to_fit();

@@ -9,11 +9,19 @@ namespace ti {
 
 using KernelFn = void (*)(KArgs);
 
-// layout: 0 heap, 1 explicit, 2 compact, 3 binned heap.  fl: feature image in
+// layout: 0 heap, 1 explicit, 2 compact, 3 binned heap, 4 binned explicit.  fl: feature image in
 // LDS; z: LightGBM zero rule; b16 / pf: binned heap bin width and prefetch
 // depth.
 template <typename XT, typename ACC, int KMAX>
 KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
+  if (layout == 4) {
+    if constexpr (sizeof(ACC) == 8) {
+      if (z) return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, true>
+                        : bexplicit_predict_kernel<XT, ACC, KMAX, false, true>;
+    }
+    return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, false>
+               : bexplicit_predict_kernel<XT, ACC, KMAX, false, false>;
+  }
   if (layout == 3) {
     if (b16) return pf <= 4 ? bheap_predict_kernel<XT, ACC, KMAX, true, 4>
                             : bheap_predict_kernel<XT, ACC, KMAX, true, 8>;

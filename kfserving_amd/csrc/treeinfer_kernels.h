@@ -570,6 +570,72 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
   return *flag != 0;
 }
 
+// Bin the tile without a temp area: every lane loads its own row's values
+// straight from global memory (neighbouring lanes share the row's cache
+// lines) and searches them as stage_bins does.  For kernels whose LDS holds
+// nothing else (the binned explicit kernel), so the bin image alone sets the
+// workgroups per CU.  Ends in a barrier; returns the tile's NaN flag.
+template <typename XT, bool B16>
+__device__ __forceinline__ bool stage_bins_rows(volatile int* flag, const KArgs& a, int64_t row0,
+                                                int R, int tid) {
+  using BT = BinTraits<B16>;
+  constexpr int P = BT::P;
+  constexpr int Q = 8;
+  const XT* tbl = static_cast<const XT*>(a.bin_tbl);
+  const int F = a.n_features;
+  const int FC = F < a.n_cols ? F : a.n_cols;
+  const int L = a.bin_L;
+  const uint32_t tsz = 1u << L;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  const XT* xr = static_cast<const XT*>(a.X) + (live ? row : a.n_rows - 1) * a.row_stride;
+  bool has_nan = false;
+  if (tid == 0) *flag = 0;
+  for (int f0 = 0; f0 < F; f0 += Q) {
+    XT x[Q];
+    const XT* tq[Q];
+    uint32_t k[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int f = f0 + q < F ? f0 + q : F - 1;
+      x[q] = f0 + q < FC ? zero_map(xr[f], a.lgb_zero_map) : nan_value<XT>();
+      tq[q] = tbl + (size_t)f * tsz;
+      k[q] = 1u;
+    }
+    for (int s = 0; s < L; ++s) {
+      XT e[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) e[q] = tq[q][k[q]];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
+    }
+    uint32_t w[Q / P];
+#pragma unroll
+    for (int j = 0; j < Q / P; ++j) w[j] = 0u;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const bool nan = x[q] != x[q];
+      has_nan |= nan && (f0 + q < F);
+      const uint32_t b = nan ? BT::kNan : 1u + k[q] - tsz;
+      w[q / P] |= b << ((q % P) * (32 / P));
+    }
+#pragma unroll
+    for (int j = 0; j < Q / P; ++j) {
+      const int word = f0 / P + j;
+      if (word < a.bin_words) {
+        __attribute__((address_space(3))) uint32_t* dst =
+            reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+                static_cast<uintptr_t>((uint32_t)(word * R + tid) * 4u));
+        *dst = w[j];
+      }
+    }
+  }
+  __syncthreads();   // flag = 0 is visible before any lane sets it
+  if (has_nan && live) *flag = 1;
+  __syncthreads();
+  return *flag != 0;
+}
+
 // Walk one LDS stage of binned complete trees.  A tree record is 2^D u32
 // entries (1-based heap: node i has children 2i and 2i+1; entry 0 unused),
 // then 2^D * leaf_width leaves (ACC).  At each level a lane issues the bin
@@ -898,6 +964,81 @@ __global__ void __launch_bounds__(512) explicit_predict_kernel(const KArgs a) {
         bool l = go_left<ZERO>(x, thr[q], nd[q].y);
         if (a.cat_words != nullptr && (nd[q].y & kMetaCat))   // uniform test, then rare branch
           l = cat_left(a.cat_words + nd[q].x, (double)x);
+        const int32_t next = l ? (int32_t)nd[q].z : (int32_t)nd[q].w;
+        c[q] = c[q] < 0 ? c[q] : next;
+        active |= c[q] >= 0;
+      }
+      if (__ballot(active) == 0) break;
+    }
+#pragma unroll
+    for (int q = 0; q < kExpIlp; ++q) {
+      const int t = t0 + q;
+      if (t < T) {
+        const int64_t lb = a.leaf_base[t];
+        if (want_leaf) {
+          if (live) out_leaf[row * T + t] = a.exp_leaf_ids[lb + (~c[q])];
+        } else {
+          add_leaf<ACC, KMAX>(acc, leaves + lb * a.leaf_width, ~c[q], a.leaf_width,
+                              a.tree_group[t]);
+        }
+      }
+    }
+  }
+  if (!live || want_leaf) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
+// ----------------------------------------------------- binned explicit kernel
+// The explicit kernel on a rank-binned feature image (any tree shape, nodes
+// in global memory).  A node is {rank | zbin << 16, offset | NaN-left (31) |
+// zero-flip (30), left, right}; offset is the feature's byte offset in the
+// bin image (without the lane part).  Split rule on bins (treeinfer.hip,
+// collect_ranks): left iff b <= rank, flipped when b == zbin (exact 0 on a
+// LightGBM zero-missing node; zbin = 0 on other nodes, and bins are >= 1),
+// and NaN (the top code) takes the NaN-left bit.
+template <typename XT, typename ACC, int KMAX, bool B16, bool ZERO>
+__global__ void __launch_bounds__(512) bexplicit_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  using BT = BinTraits<B16>;
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  const bool tile_nan = stage_bins_rows<XT, B16>(flag, a, row0, R, tid);
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  const int T = a.n_trees;
+  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
+  int32_t* out_leaf = static_cast<int32_t*>(a.out);
+  const ACC* leaves = static_cast<const ACC*>(a.leaves);
+
+  ACC acc[KMAX];
+  init_acc(acc, a);
+
+  for (int t0 = 0; t0 < T; t0 += kExpIlp) {
+    int64_t nb[kExpIlp];
+    int32_t c[kExpIlp];
+#pragma unroll
+    for (int q = 0; q < kExpIlp; ++q) {
+      const int tq = (t0 + q) < T ? (t0 + q) : (T - 1);
+      nb[q] = a.node_base[tq];
+      c[q] = a.root[tq];
+    }
+    for (;;) {
+      u32x4 nd[kExpIlp];
+#pragma unroll
+      for (int q = 0; q < kExpIlp; ++q)
+        nd[q] = *reinterpret_cast<const u32x4*>(a.nodes + nb[q] + (c[q] < 0 ? 0 : c[q]));
+      uint32_t b[kExpIlp];
+#pragma unroll
+      for (int q = 0; q < kExpIlp; ++q) b[q] = lds_bin<B16>((nd[q].y & kMetaFeatMask) | lane_off);
+      bool active = false;
+#pragma unroll
+      for (int q = 0; q < kExpIlp; ++q) {
+        bool l = b[q] <= (nd[q].x & 0xFFFFu);
+        if (ZERO) l = l != (b[q] == (nd[q].x >> 16));
+        if (tile_nan && b[q] == BT::kNan) l = (int32_t)nd[q].y < 0;
         const int32_t next = l ? (int32_t)nd[q].z : (int32_t)nd[q].w;
         c[q] = c[q] < 0 ? c[q] : next;
         active |= c[q] >= 0;
