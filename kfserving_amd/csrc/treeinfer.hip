@@ -179,6 +179,7 @@ struct ti_forest {
     int32_t rows = 256;
     int32_t words = 0;
   } bx[2];
+  int32_t bx_ilp = 4;               // trees per lane in lockstep (4 or 8)
   std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
   // host images (kept until upload)
   std::vector<unsigned char> h_heap32, h_heap64;
@@ -801,11 +802,11 @@ KernelFn select_bheap(int xdt, int accum, int K, bool b16, int pf) {
   return ti::kernels_df(3, K, true, false, b16, pf);
 }
 
-KernelFn select_bexplicit(int xdt, int accum, int K, bool b16, bool z) {
-  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(4, K, true, z, b16, 0);
-  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(4, K, true, z, b16, 0);
-  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(4, K, true, z, b16, 0);
-  return ti::kernels_df(4, K, true, z, b16, 0);
+KernelFn select_bexplicit(int xdt, int accum, int K, bool b16, bool z, int ilp) {
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(4, K, true, z, b16, ilp);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(4, K, true, z, b16, ilp);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(4, K, true, z, b16, ilp);
+  return ti::kernels_df(4, K, true, z, b16, ilp);
 }
 
 std::mutex g_attr_mu;
@@ -980,7 +981,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.bin_L = bx.L;
     a.bin_words = bx.words;
     lds = feat_bytes + 16;
-    KernelFn fn = select_bexplicit(xdt, f->accum, f->K, bx.b16 != 0, f->zero_rule != 0);
+    KernelFn fn = select_bexplicit(xdt, f->accum, f->K, bx.b16 != 0, f->zero_rule != 0, f->bx_ilp);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -1202,6 +1203,36 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
       if (pack_bexplicit<float>(desc, f.get(), &f->bx[0]) &&
           pack_bexplicit<double>(desc, f.get(), &f->bx[1])) {
         f->layout = 4;
+        // Tree ILP from the mean leaf depth: forests whose paths are short on
+        // average (leaf-wise, C3: mean leaf depth ~9) need 8 trees in flight
+        // to cover the L2 latency (measured 8.97 vs 10.8 ms at 4); deep
+        // balanced forests (sklearn depth 16, C4) are faster at 4 (3.46 vs
+        // 3.61 ms at 8), where a group's deepest path costs more.
+        double sum = 0;
+        int64_t n_leaf = 0;
+        std::vector<int32_t> dep;
+        for (int t = 0; t < desc->n_trees; ++t) {
+          const int64_t b = desc->tree_offset[t];
+          const int32_t n = static_cast<int32_t>(desc->tree_offset[t + 1] - b);
+          dep.assign(n, 0);
+          std::vector<int32_t> q(1, 0);   // breadth-first: a parent's depth is set first
+          for (size_t qi = 0; qi < q.size(); ++qi) {
+            const int32_t v = q[qi];
+            const int64_t g = b + v;
+            if (desc->feature[g] < 0) {
+              sum += dep[v];
+              ++n_leaf;
+            } else {
+              dep[desc->left[g]] = dep[desc->right[g]] = dep[v] + 1;
+              q.push_back(desc->left[g]);
+              q.push_back(desc->right[g]);
+            }
+          }
+        }
+        const double mean_depth = n_leaf ? sum / n_leaf : 0.0;
+        f->bx_ilp = mean_depth < 12.0 ? 8 : 4;
+        const int force_ilp = env_int("TI_BEXP_ILP", 0);
+        if (force_ilp > 0) f->bx_ilp = force_ilp >= 8 ? 8 : 4;
       } else {
         for (auto& bx : f->bx) bx = ti_forest::BinExplicit();
       }

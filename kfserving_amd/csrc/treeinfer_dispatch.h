@@ -14,13 +14,19 @@ using KernelFn = void (*)(KArgs);
 // depth.
 template <typename XT, typename ACC, int KMAX>
 KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
-  if (layout == 4) {
+  if (layout == 4) {   // pf carries the tree ILP (4 or 8)
     if constexpr (sizeof(ACC) == 8) {
-      if (z) return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, true>
-                        : bexplicit_predict_kernel<XT, ACC, KMAX, false, true>;
+      if (z) {
+        if (pf >= 8) return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, true, 8>
+                                : bexplicit_predict_kernel<XT, ACC, KMAX, false, true, 8>;
+        return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, true, 4>
+                   : bexplicit_predict_kernel<XT, ACC, KMAX, false, true, 4>;
+      }
     }
-    return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, false>
-               : bexplicit_predict_kernel<XT, ACC, KMAX, false, false>;
+    if (pf >= 8) return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, false, 8>
+                            : bexplicit_predict_kernel<XT, ACC, KMAX, false, false, 8>;
+    return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, false, 4>
+               : bexplicit_predict_kernel<XT, ACC, KMAX, false, false, 4>;
   }
   if (layout == 3) {
     if (b16) return pf <= 4 ? bheap_predict_kernel<XT, ACC, KMAX, true, 4>

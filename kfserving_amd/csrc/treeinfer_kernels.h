@@ -36,6 +36,9 @@
 #ifndef TI_ASM_STEP
 #define TI_ASM_STEP 1   // binned heap: hand-scheduled compare/select/carry step
 #endif
+#ifndef TI_EXP_ILP
+#define TI_EXP_ILP 4    // trees walked concurrently per lane (explicit kernels)
+#endif
 #ifndef TI_BTILP
 #define TI_BTILP 4      // trees walked concurrently per lane (binned heap)
 #endif
@@ -51,7 +54,7 @@ constexpr uint32_t kMetaCat = 0x20000000u;        // explicit layout: categorica
 constexpr uint32_t kMetaFeatMask = 0x00FFFFFFu;
 constexpr int kMaxGroups = 16;
 constexpr uint32_t kCptLeaf = 512u;       // compact child code >= 512: leaf (code - 512)
-constexpr int kExpIlp = 4;                // trees per lane in the global explicit kernel
+constexpr int kExpIlp = TI_EXP_ILP;       // trees per lane in the global explicit kernels
 constexpr int kTilp = TI_TILP;
 constexpr int kBTilp = TI_BTILP;
 constexpr int kPf = TI_PF;
@@ -995,8 +998,11 @@ __global__ void __launch_bounds__(512) explicit_predict_kernel(const KArgs a) {
 // bin image (without the lane part).  Split rule on bins (treeinfer.hip,
 // collect_ranks): left iff b <= rank, flipped when b == zbin (exact 0 on a
 // LightGBM zero-missing node; zbin = 0 on other nodes, and bins are >= 1),
-// and NaN (the top code) takes the NaN-left bit.
-template <typename XT, typename ACC, int KMAX, bool B16, bool ZERO>
+// and NaN (the top code) takes the NaN-left bit.  ILP trees are walked in
+// lockstep per lane: more of them hide more L2 latency but wait longer for the
+// deepest path of the group (the host picks 8 for shallow-on-average forests,
+// 4 for deep balanced ones).
+template <typename XT, typename ACC, int KMAX, bool B16, bool ZERO, int ILP>
 __global__ void __launch_bounds__(512) bexplicit_predict_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using BT = BinTraits<B16>;
@@ -1016,26 +1022,26 @@ __global__ void __launch_bounds__(512) bexplicit_predict_kernel(const KArgs a) {
   ACC acc[KMAX];
   init_acc(acc, a);
 
-  for (int t0 = 0; t0 < T; t0 += kExpIlp) {
-    int64_t nb[kExpIlp];
-    int32_t c[kExpIlp];
+  for (int t0 = 0; t0 < T; t0 += ILP) {
+    int64_t nb[ILP];
+    int32_t c[ILP];
 #pragma unroll
-    for (int q = 0; q < kExpIlp; ++q) {
+    for (int q = 0; q < ILP; ++q) {
       const int tq = (t0 + q) < T ? (t0 + q) : (T - 1);
       nb[q] = a.node_base[tq];
       c[q] = a.root[tq];
     }
     for (;;) {
-      u32x4 nd[kExpIlp];
+      u32x4 nd[ILP];
 #pragma unroll
-      for (int q = 0; q < kExpIlp; ++q)
+      for (int q = 0; q < ILP; ++q)
         nd[q] = *reinterpret_cast<const u32x4*>(a.nodes + nb[q] + (c[q] < 0 ? 0 : c[q]));
-      uint32_t b[kExpIlp];
+      uint32_t b[ILP];
 #pragma unroll
-      for (int q = 0; q < kExpIlp; ++q) b[q] = lds_bin<B16>((nd[q].y & kMetaFeatMask) | lane_off);
+      for (int q = 0; q < ILP; ++q) b[q] = lds_bin<B16>((nd[q].y & kMetaFeatMask) | lane_off);
       bool active = false;
 #pragma unroll
-      for (int q = 0; q < kExpIlp; ++q) {
+      for (int q = 0; q < ILP; ++q) {
         bool l = b[q] <= (nd[q].x & 0xFFFFu);
         if (ZERO) l = l != (b[q] == (nd[q].x >> 16));
         if (tile_nan && b[q] == BT::kNan) l = (int32_t)nd[q].y < 0;
@@ -1046,7 +1052,7 @@ __global__ void __launch_bounds__(512) bexplicit_predict_kernel(const KArgs a) {
       if (__ballot(active) == 0) break;
     }
 #pragma unroll
-    for (int q = 0; q < kExpIlp; ++q) {
+    for (int q = 0; q < ILP; ++q) {
       const int t = t0 + q;
       if (t < T) {
         const int64_t lb = a.leaf_base[t];
