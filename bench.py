@@ -42,6 +42,9 @@ def parse_args():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--rows", type=int, default=ROWS)
+    p.add_argument("--nan-variant", type=float, default=0.01,
+                   help="also time the same batch with this fraction of NaN features "
+                        "(SURVEY.md 8(d) C2 1%%-NaN variant; 0 = skip)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="target CPU work for the cpu_baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -220,6 +223,28 @@ def main():
     total_rows = rows * world * args.steps
     value = total_rows / wall
 
+    nan_variant = None
+    if args.nan_variant > 0 and rank == 0:
+        # same shape, seed 1, NaN at random positions: every tile takes the
+        # kernel's NaN-checking path (not part of the headline value)
+        Xn_host = np.random.default_rng(1).standard_normal((rows, N_FEAT), dtype=np.float32)
+        Xn_host[np.random.default_rng(2).random(Xn_host.shape) < args.nan_variant] = np.nan
+        Xn = torch.from_numpy(Xn_host).to(f"cuda:{local_rank}")
+        for _ in range(2):
+            dev.predict_device(Xn.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
+                               out.data_ptr(), rows, slot=0, stream=sh)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            dev.predict_device(Xn.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
+                               out.data_ptr(), rows, slot=0, stream=sh)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        nms = e0.elapsed_time(e1) / args.steps
+        nan_variant = {"nan_fraction": args.nan_variant, "kernel_ms": nms,
+                       "rows_per_s": rows / (nms * 1e-3)}
+        del Xn
+
     if rank == 0:
         visits = N_TREES * DEPTH                     # complete trees: every row visits D nodes
         b_visit = 8 * visits + 4 * N_FEAT + 4        # SURVEY.md 8(d) B_visit
@@ -267,6 +292,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "batched_latency": latency,
+            "nan_variant": nan_variant,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,15 +1,24 @@
-"""Device-resident throughput of the non-headline BASELINE.json configs on one
-GPU (the headline C2 is bench.py).  One JSON line per config:
+"""Device-resident throughput of the non-headline BASELINE.json configs at
+their named sizes (the headline C2 is bench.py).  One JSON line per config:
 
-  C3  LightGBM leaf-wise, 1000 trees x 255 leaves, 100 features (f32 input;
-      BASELINE: 100M rows sharded over 1-8 GPUs -- measured per GPU on a
-      --rows3 batch), CPU baseline = oracle/c/tree_port.c lightgbm restatement.
+  C3  LightGBM leaf-wise, 1000 trees x 255 leaves, 100 features, float32
+      input; 100M rows (BASELINE configs[2]) generated on the device, row-
+      sharded over the ranks of a torchrun launch (strong scaling: the 100M
+      rows are split).  CPU baseline: oracle/c/tree_port.c, the lightgbm
+      predict loop restated in C/OpenMP (lightgbm is not installed).
   C4  sklearn RandomForestRegressor(200, max_depth=16, max_features=1/3),
       64 features, fitted here on N(0,1) [--fit-rows x 64] with a nonlinear
-      target; predict on a --rows4 batch (BASELINE: 10M rows).  CPU baseline =
-      sklearn's own predict(n_jobs=all threads) on a bounded sample.
+      target; predict 10M rows (BASELINE configs[3]).  CPU baseline: sklearn's
+      own predict (n_jobs = the host threads) on a bounded sample.
+
+Each line carries a roofline block in the SURVEY.md 8(d) byte model for the
+explicit layouts: B_visit = 16 B x V + 4 B x F + out bytes per row (V = node
+visits per row, measured from the leaves reached on a sample), divided by the
+kernel time, against 8 TB/s HBM; and a parity spot check of the first rows of
+the device batch against the oracle (C3) / sklearn itself (C4).
 
 Usage: python scripts/bench_configs.py [--configs c3,c4] [--rows3 N] [--rows4 N]
+       python -m torch.distributed.run --nproc-per-node G scripts/bench_configs.py ...
 """
 import argparse
 import json
@@ -22,15 +31,40 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+HBM_PEAK = 8.0e12
+
+
+def dist_info():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def max_over_ranks(v):
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shard(total, world, rank):
+    per = (total + world - 1) // world
+    lo = min(total, rank * per)
+    return lo, min(total, lo + per)
 
 
 def time_device(dev, X_t, out_t, rows, cols, kind, xdt, steps, warmup):
     import torch
+    import torch.distributed as dist
     stream = torch.cuda.current_stream()
     for _ in range(warmup):
         dev.predict_device(X_t.data_ptr(), xdt, rows, cols, cols, kind, out_t.data_ptr(),
                            out_t.numel(), stream=stream.cuda_stream)
     torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
@@ -39,44 +73,23 @@ def time_device(dev, X_t, out_t, rows, cols, kind, xdt, steps, warmup):
                            out_t.numel(), stream=stream.cuda_stream)
     e1.record(stream)
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    return rows * steps / wall, e0.elapsed_time(e1) / steps
+    if dist.is_initialized():
+        dist.barrier()
+    wall = max_over_ranks(time.perf_counter() - t0)
+    return wall / steps, e0.elapsed_time(e1) / steps
 
 
-def c3(args):
+def device_normal(rows, cols, seed):
+    """X ~ N(0,1) float32 generated on the device in 8M-row chunks (seed, chunk)."""
     import torch
-    from kfserving_amd.engine import DeviceForest
-    from kfserving_amd.formats import lightgbm_format as lf
-    from kfserving_amd.forest import OUT_MARGIN, TI_F32
-    from oracle import port
-    F = args.f3
-    trees = lf.synthetic_leafwise_trees(1000, 255, F, seed=1)
-    with tempfile.TemporaryDirectory() as d:
-        p = os.path.join(d, "model.txt")
-        lf.write_lightgbm_text(p, trees, F, "binary sigmoid:1")
-        f = lf.load_lightgbm_model(p)
-    depths = f.depths()
-    dev = DeviceForest(f, [0])
-    rows = args.rows3
-    X = np.random.default_rng(3).standard_normal((rows, F), dtype=np.float32)
-    Xt = torch.from_numpy(X).cuda()
-    out = torch.empty(rows, dtype=torch.float64, device="cuda")
-    rate, kms = time_device(dev, Xt, out, rows, F, OUT_MARGIN, TI_F32, args.steps, 2)
-    # node visits per row, measured from the leaves reached on a sample
-    from tests import canon_eval
-    lv = canon_eval.leaves(f, X[:2000])
-    node_depth = _node_depths(f)
-    visits = float(np.mean(np.sum(node_depth[f.tree_offset[:-1][None, :] + lv], axis=1)))
-    n = min(rows, 50_000)
-    t0 = time.perf_counter()
-    port.lgb_predict_raw(trees, 1, F, X[:n].astype(np.float64))
-    cpu = n / (time.perf_counter() - t0)
-    return {"config": f"C3 LightGBM leaf-wise 1000x255 leaves, {F} feat, f32 input",
-            "rows": rows, "rows_per_s": rate, "kernel_ms": kms, "layout": dev.info()["layout"],
-            "max_depth": int(depths.max()), "mean_tree_depth": float(depths.mean()),
-            "node_visits_per_row": visits,
-            "cpu_baseline": {"rows_per_s": cpu, "kind": "port", "threads": port.num_threads(),
-                             "sample_rows": n}}
+    X = torch.empty((rows, cols), dtype=torch.float32, device="cuda")
+    chunk = 8 << 20
+    for i, lo in enumerate(range(0, rows, chunk)):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(seed * 1000003 + i)
+        hi = min(rows, lo + chunk)
+        X[lo:hi] = torch.randn((hi - lo, cols), generator=g, device="cuda", dtype=torch.float32)
+    return X
 
 
 def _node_depths(f):
@@ -92,7 +105,63 @@ def _node_depths(f):
     return d
 
 
-def c4(args):
+def visits_per_row(f, X_sample):
+    from tests import canon_eval
+    lv = canon_eval.leaves(f, X_sample)
+    node_depth = _node_depths(f)
+    return float(np.mean(np.sum(node_depth[f.tree_offset[:-1][None, :] + lv], axis=1)))
+
+
+def roofline(visits, n_feat, out_bytes, rows, kernel_ms):
+    b = 16 * visits + 4 * n_feat + out_bytes
+    achieved = b * rows / (kernel_ms * 1e-3)
+    return {"bound": "hbm", "bytes_per_row_visit_model": b, "achieved": achieved / 1e9,
+            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
+            "compulsory_GBps": (4 * n_feat + out_bytes) * rows / (kernel_ms * 1e-3) / 1e9}
+
+
+def c3(args, world, rank):
+    import torch
+    from kfserving_amd.engine import DeviceForest
+    from kfserving_amd.formats import lightgbm_format as lf
+    from kfserving_amd.forest import OUT_MARGIN, TI_F32
+    from oracle import port
+    F = args.f3
+    trees = lf.synthetic_leafwise_trees(1000, 255, F, seed=1)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, F, "binary sigmoid:1")
+        f = lf.load_lightgbm_model(p)
+    depths = f.depths()
+    dev = DeviceForest(f, [torch.cuda.current_device()])
+    lo, hi = shard(args.rows3, world, rank)
+    rows = hi - lo
+    X = device_normal(rows, F, seed=3 + rank)
+    out = torch.empty(rows, dtype=torch.float64, device="cuda")
+    step_s, kms = time_device(dev, X, out, rows, F, OUT_MARGIN, TI_F32, args.steps, 1)
+    if rank != 0:
+        return None
+    n_chk = min(rows, 20_000)
+    Xs = X[:n_chk].cpu().numpy()
+    exact = bool(np.array_equal(out[:n_chk].cpu().numpy(),
+                                port.lgb_predict_raw(trees, 1, F, Xs.astype(np.float64))[:, 0]))
+    visits = visits_per_row(f, Xs[:2000])
+    n = min(n_chk, 50_000)
+    t0 = time.perf_counter()
+    port.lgb_predict_raw(trees, 1, F, Xs[:n].astype(np.float64))
+    cpu = n / (time.perf_counter() - t0)
+    return {"config": f"C3 LightGBM leaf-wise 1000x255 leaves, {F} feat, f32 input",
+            "rows": args.rows3, "n_gpus": world, "rows_per_gpu": rows, "scaling": "strong",
+            "rows_per_s": args.rows3 / step_s, "step_ms": step_s * 1e3, "kernel_ms": kms,
+            "layout": dev.info()["layout"], "max_depth": int(depths.max()),
+            "mean_tree_depth": float(depths.mean()), "node_visits_per_row": visits,
+            "roofline": roofline(visits, F, 8, rows, kms),
+            "bit_exact_vs_port_first_rows": exact, "parity_rows": n_chk,
+            "cpu_baseline": {"rows_per_s": cpu, "kind": "port", "threads": port.num_threads(),
+                             "sample_rows": n}}
+
+
+def c4(args, world, rank):
     import torch
     from sklearn.ensemble import RandomForestRegressor
     from kfserving_amd.engine import DeviceForest
@@ -108,41 +177,54 @@ def c4(args):
                                 random_state=0, n_jobs=n_thr).fit(Xtr, ytr)
     fit_s = time.perf_counter() - t0
     f = forest_from_sklearn(est)
-    dev = DeviceForest(f, [0])
-    rows = args.rows4
-    X = np.random.default_rng(2).standard_normal((rows, 64), dtype=np.float32)
-    Xt = torch.from_numpy(X).cuda()
+    dev = DeviceForest(f, [torch.cuda.current_device()])
+    lo, hi = shard(args.rows4, world, rank)
+    rows = hi - lo
+    X = device_normal(rows, 64, seed=2 + rank)
     out = torch.empty(rows, dtype=torch.float64, device="cuda")
-    rate, kms = time_device(dev, Xt, out, rows, 64, OUT_PREDICT, TI_F32, args.steps, 2)
-    got = out[:4096].cpu().numpy()
+    step_s, kms = time_device(dev, X, out, rows, 64, OUT_PREDICT, TI_F32, args.steps, 1)
+    if rank != 0:
+        return None
+    Xs = X[:4096].cpu().numpy()
     est.set_params(n_jobs=1)
-    exact = bool(np.array_equal(got, est.predict(X[:4096])))
+    exact = bool(np.array_equal(out[:4096].cpu().numpy(), est.predict(Xs)))
     est.set_params(n_jobs=n_thr)
-    n = min(rows, 200_000)
+    visits = visits_per_row(f, Xs[:1000])
+    Xc = X[:min(rows, 200_000)].cpu().numpy()
     t0 = time.perf_counter()
-    est.predict(X[:n])
-    cpu = n / (time.perf_counter() - t0)
+    est.predict(Xc)
+    cpu = Xc.shape[0] / (time.perf_counter() - t0)
     return {"config": "C4 sklearn RandomForestRegressor 200 x depth16, 64 feat",
-            "rows": rows, "rows_per_s": rate, "kernel_ms": kms, "layout": dev.info()["layout"],
-            "nodes_per_tree": f.n_nodes / f.n_trees, "fit_s": fit_s,
-            "bit_exact_vs_sklearn_4096": exact,
+            "rows": args.rows4, "n_gpus": world, "rows_per_gpu": rows, "scaling": "strong",
+            "rows_per_s": args.rows4 / step_s, "step_ms": step_s * 1e3, "kernel_ms": kms,
+            "layout": dev.info()["layout"], "nodes_per_tree": f.n_nodes / f.n_trees,
+            "node_visits_per_row": visits, "roofline": roofline(visits, 64, 8, rows, kms),
+            "fit_s": fit_s, "bit_exact_vs_sklearn_4096": exact,
             "cpu_baseline": {"rows_per_s": cpu, "kind": "reference (sklearn 1.7.2 predict)",
-                             "threads": n_thr, "sample_rows": n}}
+                             "threads": n_thr, "sample_rows": Xc.shape[0]}}
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--configs", default="c3,c4")
-    p.add_argument("--rows3", type=int, default=1_000_000)
+    p.add_argument("--rows3", type=int, default=100_000_000)
     p.add_argument("--f3", type=int, default=100, help="C3 feature count (BASELINE: 100)")
-    p.add_argument("--rows4", type=int, default=1_000_000)
+    p.add_argument("--rows4", type=int, default=10_000_000)
     p.add_argument("--fit-rows", type=int, default=200_000)
-    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--steps", type=int, default=3)
     args = p.parse_args()
     import torch  # noqa: F401  (one HIP runtime: torch's, loaded first)
+    import torch.distributed as dist
+    world, rank, local = dist_info()
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
     for c in args.configs.split(","):
-        res = {"c3": c3, "c4": c4}[c.strip()](args)
-        print(json.dumps(res), flush=True)
+        res = {"c3": c3, "c4": c4}[c.strip()](args, world, rank)
+        if res is not None:
+            print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
