@@ -141,6 +141,11 @@ struct DeviceForest {
 }  // namespace
 
 struct ti_forest {
+  // Forests with more than kMaxGroups outputs are split into parts of at most
+  // kMaxGroups groups each (see create_chunked); the parent holds the parts.
+  std::vector<std::unique_ptr<ti_forest>> parts;
+  std::vector<int32_t> part_k0;                  // first output group of each part
+  std::vector<std::vector<int32_t>> part_trees;  // original tree index of each part tree
   int32_t T = 0, F = 0, K = 1, LW = 1, accum = TI_F32, base_first = 1, lgb_zero_map = 0;
   int32_t zero_rule = 0, transform = TI_TRANSFORM_IDENTITY;
   double tparam = 1.0, divisor = 1.0;
@@ -254,8 +259,7 @@ int validate(const ti_forest_desc* d, std::vector<int>* depth_out) {
   if (d->n_features <= 0 || d->n_features > (1 << 24))
     return fail(TI_ERR_INVALID, "n_features out of range");
   if (d->n_groups <= 0) return fail(TI_ERR_INVALID, "n_groups must be > 0");
-  if (d->n_groups > ti::kMaxGroups)
-    return fail(TI_ERR_UNSUPPORTED, "n_groups > 16 is not supported by this build");
+  if (d->n_groups > (1 << 20)) return fail(TI_ERR_UNSUPPORTED, "n_groups > 2^20");
   if (d->leaf_width != 1 && d->leaf_width != d->n_groups)
     return fail(TI_ERR_INVALID, "leaf_width must be 1 or n_groups");
   if (d->accum_dtype != TI_F32 && d->accum_dtype != TI_F64)
@@ -1042,8 +1046,11 @@ int grow(void** buf, size_t* cap, size_t need, bool pinned = false) {
   return TI_OK;
 }
 
-int predict_shard(ti_forest* f, DeviceForest& d, const unsigned char* X, int xdt, int64_t rows,
-                  int32_t cols, int64_t stride, int kind, unsigned char* out) {
+int launch_any(ti_forest* f, int slot, const void* X, int xdt, int64_t rows, int32_t cols,
+               int64_t stride, int kind, void* out, hipStream_t stream);
+
+int predict_shard(ti_forest* f, int slot, DeviceForest& d, const unsigned char* X, int xdt,
+                  int64_t rows, int32_t cols, int64_t stride, int kind, unsigned char* out) {
   std::lock_guard<std::mutex> lk(d.mu);
   TI_HIP(hipSetDevice(d.device));
   const size_t xs = dtype_size(xdt);
@@ -1060,11 +1067,234 @@ int predict_shard(ti_forest* f, DeviceForest& d, const unsigned char* X, int xdt
   // PCIe rate whatever kind of host memory the caller holds
   std::memcpy(d.hx_pin, X, x_bytes);
   TI_HIP(hipMemcpyAsync(d.x_buf, d.hx_pin, x_bytes, hipMemcpyHostToDevice, d.stream));
-  if ((rc = launch(f, d, d.x_buf, xdt, rows, cols, stride, kind, d.out_buf, d.stream))) return rc;
+  if ((rc = launch_any(f, slot, d.x_buf, xdt, rows, cols, stride, kind, d.out_buf, d.stream)))
+    return rc;
   TI_HIP(hipMemcpyAsync(d.ho_pin, d.out_buf, out_bytes, hipMemcpyDeviceToHost, d.stream));
   TI_HIP(hipStreamSynchronize(d.stream));
   std::memcpy(out, d.ho_pin, out_bytes);
   return TI_OK;
+}
+
+// ------------------------------------------------- more than 16 output groups
+// Output transform over [rows, K] margins for forests split into group parts
+// (the fused epilogue covers K <= kMaxGroups).  Same arithmetic as
+// ti::finish_row: softmax with the maximum in ACC and the sum in double,
+// first-maximum argmax.
+template <typename ACC>
+__global__ void transform_rows_kernel(const ACC* __restrict__ m, int64_t rows, int K, int tr,
+                                      double param, ACC* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const ACC* v = m + r * K;
+  if (tr == TI_TRANSFORM_ARGMAX) {
+    int best = 0;
+    for (int k = 1; k < K; ++k)
+      if (v[best] < v[k]) best = k;
+    out[r] = (ACC)best;
+    return;
+  }
+  ACC* o = out + r * K;
+  if (tr == TI_TRANSFORM_SOFTMAX) {
+    ACC wmax = v[0];
+    for (int k = 1; k < K; ++k) wmax = (v[k] < wmax) ? wmax : v[k];
+    double wsum = 0.0;
+    for (int k = 0; k < K; ++k) wsum += ti::t_exp(v[k] - wmax);
+    for (int k = 0; k < K; ++k) o[k] = ti::t_exp(v[k] - wmax) / (ACC)wsum;
+    return;
+  }
+  for (int k = 0; k < K; ++k) {
+    ACC x = v[k];
+    switch (tr) {
+      case TI_TRANSFORM_SIGMOID: x = ACC(1) / (ACC(1) + ti::t_exp(-((ACC)param * x))); break;
+      case TI_TRANSFORM_HINGE: x = x > ACC(0) ? ACC(1) : ACC(0); break;
+      case TI_TRANSFORM_EXP: x = ti::t_exp(x); break;
+      case TI_TRANSFORM_SIGNSQUARE: x = (ACC)((x > ACC(0)) - (x < ACC(0))) * x * x; break;
+      case TI_TRANSFORM_LOG1PEXP: x = ti::t_log1p(ti::t_exp(x)); break;
+      default: break;
+    }
+    o[k] = x;
+  }
+}
+
+// dst[r, map[j]] = src[r, j] for the leaf-id columns of one part.
+__global__ void scatter_cols_kernel(const int32_t* __restrict__ src, int64_t rows, int tc,
+                                    const int32_t* __restrict__ map, int T,
+                                    int32_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * tc) return;
+  const int64_t r = i / tc;
+  const int j = (int)(i - r * tc);
+  dst[r * T + map[j]] = src[i];
+}
+
+int launch_any(ti_forest* f, int slot, const void* X, int xdt, int64_t rows, int32_t cols,
+               int64_t stride, int kind, void* out, hipStream_t stream);
+
+// Device path of a chunked forest: each part writes its margin columns (or
+// leaf-id columns) through a stream-ordered scratch buffer, then the output
+// transform runs over the assembled [rows, K] margins.
+int launch_chunked(ti_forest* f, int slot, const void* X, int xdt, int64_t rows, int32_t cols,
+                   int64_t stride, int kind, void* out, hipStream_t stream) {
+  const size_t as = f->accum == TI_F64 ? 8 : 4;
+  const int threads = 256;
+  if (kind == TI_OUTPUT_LEAF && f->LW != 1)   // vector leaves: every part holds every tree
+    return launch_any(f->parts[0].get(), slot, X, xdt, rows, cols, stride, kind, out, stream);
+  void* tmp = nullptr;
+  void* marg = nullptr;
+  int32_t* dmap = nullptr;
+  int rc = TI_OK;
+  size_t tmp_bytes = 0;
+  for (auto& p : f->parts)
+    tmp_bytes = std::max(tmp_bytes, static_cast<size_t>(rows) *
+                                        (kind == TI_OUTPUT_LEAF ? 4 * p->T : as * p->K));
+  TI_HIP(hipMallocAsync(&tmp, tmp_bytes, stream));
+  const bool transform = kind == TI_OUTPUT_PREDICT && f->transform != TI_TRANSFORM_IDENTITY;
+  if (transform) {
+    if (hipMallocAsync(&marg, static_cast<size_t>(rows) * f->K * as, stream) != hipSuccess) {
+      (void)hipFreeAsync(tmp, stream);
+      return fail(TI_ERR_NOMEM, "margin scratch allocation failed");
+    }
+  }
+  void* mdst = transform ? marg : out;
+  for (size_t c = 0; c < f->parts.size() && rc == TI_OK; ++c) {
+    ti_forest* p = f->parts[c].get();
+    if (kind == TI_OUTPUT_LEAF) {
+      rc = launch_any(p, slot, X, xdt, rows, cols, stride, kind, tmp, stream);
+      if (rc) break;
+      const std::vector<int32_t>& map = f->part_trees[c];
+      if (hipMallocAsync(reinterpret_cast<void**>(&dmap), map.size() * 4, stream) != hipSuccess ||
+          hipMemcpyAsync(dmap, map.data(), map.size() * 4, hipMemcpyHostToDevice, stream) !=
+              hipSuccess) {
+        rc = fail(TI_ERR_DEVICE, "leaf map upload failed");
+        break;
+      }
+      const int64_t n = rows * p->T;
+      hipLaunchKernelGGL(scatter_cols_kernel, dim3(static_cast<unsigned>((n + threads - 1) / threads)),
+                         dim3(threads), 0, stream, static_cast<const int32_t*>(tmp), rows, p->T,
+                         dmap, f->T, static_cast<int32_t*>(out));
+      (void)hipFreeAsync(dmap, stream);
+      dmap = nullptr;
+    } else {
+      rc = launch_any(p, slot, X, xdt, rows, cols, stride, TI_OUTPUT_MARGIN, tmp, stream);
+      if (rc) break;
+      if (hipMemcpy2DAsync(static_cast<unsigned char*>(mdst) + f->part_k0[c] * as, f->K * as, tmp,
+                           p->K * as, p->K * as, rows, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+        rc = fail(TI_ERR_DEVICE, "margin column copy failed");
+    }
+  }
+  if (rc == TI_OK && transform) {
+    const unsigned grid = static_cast<unsigned>((rows + threads - 1) / threads);
+    if (f->accum == TI_F64)
+      hipLaunchKernelGGL(transform_rows_kernel<double>, dim3(grid), dim3(threads), 0, stream,
+                         static_cast<const double*>(marg), rows, f->K, f->transform, f->tparam,
+                         static_cast<double*>(out));
+    else
+      hipLaunchKernelGGL(transform_rows_kernel<float>, dim3(grid), dim3(threads), 0, stream,
+                         static_cast<const float*>(marg), rows, f->K, f->transform, f->tparam,
+                         static_cast<float*>(out));
+    if (hipGetLastError() != hipSuccess) rc = fail(TI_ERR_DEVICE, "transform launch failed");
+  }
+  (void)hipFreeAsync(tmp, stream);
+  if (marg) (void)hipFreeAsync(marg, stream);
+  return rc;
+}
+
+int launch_any(ti_forest* f, int slot, const void* X, int xdt, int64_t rows, int32_t cols,
+               int64_t stride, int kind, void* out, hipStream_t stream) {
+  if (!f->parts.empty())
+    return launch_chunked(f, slot, X, xdt, rows, cols, stride, kind, out, stream);
+  return launch(f, *f->devs[slot], X, xdt, rows, cols, stride, kind, out, stream);
+}
+
+// Split a forest of K > kMaxGroups outputs into parts of at most kMaxGroups
+// groups.  Scalar leaves (leaf_width 1, XGBoost / LightGBM multiclass): a
+// part holds the trees of its groups, in their original order, so each
+// group's sum is bit-identical.  Vector leaves (sklearn classifiers): every
+// part holds every tree with its slice of the leaf vectors.
+int create_chunked(const ti_forest_desc* d, const int32_t* devices, int32_t n_devices,
+                   ti_forest** out) {
+  std::unique_ptr<ti_forest> f(new ti_forest());
+  f->T = d->n_trees;
+  f->F = d->n_features;
+  f->K = d->n_groups;
+  f->LW = d->leaf_width;
+  f->accum = d->accum_dtype;
+  f->base_first = d->base_first ? 1 : 0;
+  f->transform = d->transform;
+  f->tparam = d->transform_param;
+  f->divisor = d->average_divisor;
+  const int K = d->n_groups, LW = d->leaf_width;
+  for (int k0 = 0; k0 < K; k0 += ti::kMaxGroups) {
+    const int kc = std::min(ti::kMaxGroups, K - k0);
+    std::vector<int32_t> trees, tgrp, feat, left, right, leaf_id, cat_nw;
+    std::vector<int64_t> toff(1, 0), cat_off;
+    std::vector<double> thr, lv, base(d->base_margin + k0, d->base_margin + k0 + kc);
+    std::vector<uint8_t> flags;
+    for (int t = 0; t < d->n_trees; ++t) {
+      if (LW == 1 && (d->tree_group[t] < k0 || d->tree_group[t] >= k0 + kc)) continue;
+      trees.push_back(t);
+      tgrp.push_back(LW == 1 ? d->tree_group[t] - k0 : 0);
+      for (int64_t g = d->tree_offset[t]; g < d->tree_offset[t + 1]; ++g) {
+        feat.push_back(d->feature[g]);
+        thr.push_back(d->threshold[g]);
+        flags.push_back(d->flags[g]);
+        left.push_back(d->left[g]);
+        right.push_back(d->right[g]);
+        leaf_id.push_back(d->leaf_id[g]);
+        if (d->cat_offset) {
+          cat_off.push_back(d->cat_offset[g]);
+          cat_nw.push_back(d->cat_nwords[g]);
+        }
+        if (LW == 1) {
+          lv.push_back(d->leaf_value[g]);
+        } else {
+          for (int k = 0; k < kc; ++k) lv.push_back(d->leaf_value[g * LW + k0 + k]);
+        }
+      }
+      toff.push_back(static_cast<int64_t>(feat.size()));
+    }
+    if (trees.empty())
+      return fail(TI_ERR_UNSUPPORTED, "output groups " + std::to_string(k0) + ".." +
+                                          std::to_string(k0 + kc - 1) + " have no trees");
+    ti_forest_desc sd = *d;
+    sd.n_trees = static_cast<int32_t>(trees.size());
+    sd.n_groups = kc;
+    sd.leaf_width = LW == 1 ? 1 : kc;
+    sd.n_nodes = static_cast<int64_t>(feat.size());
+    sd.tree_offset = toff.data();
+    sd.tree_group = tgrp.data();
+    sd.feature = feat.data();
+    sd.threshold = thr.data();
+    sd.flags = flags.data();
+    sd.left = left.data();
+    sd.right = right.data();
+    sd.leaf_id = leaf_id.data();
+    sd.leaf_value = lv.data();
+    sd.base_margin = base.data();
+    sd.transform = TI_TRANSFORM_IDENTITY;
+    sd.transform_param = 1.0;
+    sd.cat_offset = d->cat_offset ? cat_off.data() : nullptr;
+    sd.cat_nwords = d->cat_offset ? cat_nw.data() : nullptr;
+    ti_forest* part = nullptr;
+    const int rc = ti_forest_create(&sd, devices, n_devices, &part);
+    if (rc) {
+      for (auto& q : f->parts) ti_forest_destroy(q.release());
+      return rc;
+    }
+    f->parts.emplace_back(part);
+    f->part_k0.push_back(k0);
+    f->part_trees.push_back(std::move(trees));
+    f->depth = std::max(f->depth, part->depth);
+  }
+  f->layout = f->parts[0]->layout;
+  *out = f.release();
+  return TI_OK;
+}
+
+// The forest whose DeviceForest (stream, staging buffers, lock) serves a slot.
+ti_forest* base_forest(ti_forest* f) {
+  while (!f->parts.empty()) f = f->parts[0].get();
+  return f;
 }
 
 }  // namespace
@@ -1096,6 +1326,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   for (int i = 0; i < n_devices; ++i)
     if (devices[i] < 0 || devices[i] >= n_visible)
       return fail(TI_ERR_INVALID, "device ordinal " + std::to_string(devices[i]) + " not visible");
+  if (desc->n_groups > ti::kMaxGroups) return create_chunked(desc, devices, n_devices, out);
 
   std::unique_ptr<ti_forest> f(new ti_forest());
   f->T = desc->n_trees;
@@ -1278,6 +1509,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
 
 int ti_forest_destroy(ti_forest* forest) {
   if (!forest) return TI_OK;
+  for (auto& p : forest->parts) ti_forest_destroy(p.release());
   for (auto& d : forest->devs) free_device(*d);
   delete forest;
   return TI_OK;
@@ -1290,8 +1522,15 @@ int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
   info->n_trees = f->T;
   info->n_groups = f->K;
   info->n_features = f->F;
-  info->n_devices = static_cast<int32_t>(f->devs.size());
-  info->device_bytes = f->devs.empty() ? 0 : f->devs[0]->bytes;
+  const ti_forest* bf = f;
+  while (!bf->parts.empty()) bf = bf->parts[0].get();
+  info->n_devices = static_cast<int32_t>(bf->devs.size());
+  info->device_bytes = 0;
+  if (f->parts.empty()) {
+    info->device_bytes = f->devs.empty() ? 0 : f->devs[0]->bytes;
+  } else {
+    for (auto& p : f->parts) info->device_bytes += p->devs.empty() ? 0 : p->devs[0]->bytes;
+  }
   info->tree_stride_bytes = f->layout == 0 ? f->stride32 : f->layout == 3 ? f->bh[0].stride : 0;
   return TI_OK;
 }
@@ -1326,13 +1565,14 @@ int ti_predict(ti_forest* f, const void* X, int32_t xdt, int64_t rows, int32_t c
                int64_t stride, int32_t kind, void* out, int64_t out_len) {
   int rc = check_call(f, X, xdt, rows, cols, stride, kind, out, out_len);
   if (rc || rows == 0) return rc;
-  const int nd = static_cast<int>(f->devs.size());
+  ti_forest* bf = base_forest(f);   // a chunked forest's parts share its device list
+  const int nd = static_cast<int>(bf->devs.size());
   const size_t xs = dtype_size(xdt);
   const size_t os = dtype_size(output_dtype(f, kind)) * output_width(f, kind);
   const int64_t per = (rows + nd - 1) / nd;
   const unsigned char* xb = static_cast<const unsigned char*>(X);
   unsigned char* ob = static_cast<unsigned char*>(out);
-  if (nd == 1) return predict_shard(f, *f->devs[0], xb, xdt, rows, cols, stride, kind, ob);
+  if (nd == 1) return predict_shard(f, 0, *bf->devs[0], xb, xdt, rows, cols, stride, kind, ob);
   std::vector<int> rcs(nd, TI_OK);
   std::vector<std::string> errs(nd);
   std::vector<std::thread> th;
@@ -1341,7 +1581,7 @@ int ti_predict(ti_forest* f, const void* X, int32_t xdt, int64_t rows, int32_t c
     const int64_t r1 = std::min(rows, r0 + per);
     if (r0 >= r1) break;
     th.emplace_back([&, i, r0, r1]() {
-      rcs[i] = predict_shard(f, *f->devs[i], xb + r0 * stride * xs, xdt, r1 - r0, cols, stride,
+      rcs[i] = predict_shard(f, i, *bf->devs[i], xb + r0 * stride * xs, xdt, r1 - r0, cols, stride,
                              kind, ob + r0 * os);
       if (rcs[i]) errs[i] = g_last_error;
     });
@@ -1357,11 +1597,12 @@ int ti_predict_device(ti_forest* f, int32_t slot, const void* X, int32_t xdt, in
                       void* stream) {
   int rc = check_call(f, X, xdt, rows, cols, stride, kind, out, out_len);
   if (rc || rows == 0) return rc;
-  if (slot < 0 || slot >= static_cast<int>(f->devs.size()))
+  ti_forest* bf = base_forest(f);
+  if (slot < 0 || slot >= static_cast<int>(bf->devs.size()))
     return fail(TI_ERR_INVALID, "device_slot out of range");
-  DeviceForest& d = *f->devs[slot];
+  DeviceForest& d = *bf->devs[slot];
   TI_HIP(hipSetDevice(d.device));
-  return launch(f, d, X, xdt, rows, cols, stride, kind, out, static_cast<hipStream_t>(stream));
+  return launch_any(f, slot, X, xdt, rows, cols, stride, kind, out, static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

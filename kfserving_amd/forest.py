@@ -48,7 +48,9 @@ MISSING_NONE = 0
 MISSING_ZERO = 1
 MISSING_NAN = 2
 
-MAX_GROUPS = 16
+# outputs per row; the library splits forests of more than 16 groups into
+# parts of at most 16 (treeinfer.hip, create_chunked)
+MAX_GROUPS = 1 << 20
 
 
 @dataclass
