@@ -93,6 +93,7 @@ extern "C" {
 #define TI_TRANSFORM_EXP         5  /* exp(x)                                */
 #define TI_TRANSFORM_SIGNSQUARE  6  /* sign(x) * x * x (LightGBM sqrt)       */
 #define TI_TRANSFORM_LOG1PEXP    7  /* log(1 + exp(x)) (LightGBM xentlambda) */
+#define TI_TRANSFORM_STEP        8  /* x >= 0 ? 1 : 0 (sklearn binary GradientBoosting label) */
 
 /* what ti_predict writes */
 #define TI_OUTPUT_MARGIN   0  /* raw score (after base/average), [rows, K]     */

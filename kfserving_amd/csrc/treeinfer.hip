@@ -264,7 +264,7 @@ int validate(const ti_forest_desc* d, std::vector<int>* depth_out) {
     return fail(TI_ERR_INVALID, "leaf_width must be 1 or n_groups");
   if (d->accum_dtype != TI_F32 && d->accum_dtype != TI_F64)
     return fail(TI_ERR_INVALID, "accum_dtype must be TI_F32 or TI_F64");
-  if (d->transform < TI_TRANSFORM_IDENTITY || d->transform > TI_TRANSFORM_LOG1PEXP)
+  if (d->transform < TI_TRANSFORM_IDENTITY || d->transform > TI_TRANSFORM_STEP)
     return fail(TI_ERR_INVALID, "unknown transform");
   if (!(d->average_divisor > 0.0)) return fail(TI_ERR_INVALID, "average_divisor must be > 0");
   if (!d->tree_offset || !d->feature || !d->threshold || !d->flags || !d->left || !d->right ||
@@ -1110,6 +1110,7 @@ __global__ void transform_rows_kernel(const ACC* __restrict__ m, int64_t rows, i
       case TI_TRANSFORM_EXP: x = ti::t_exp(x); break;
       case TI_TRANSFORM_SIGNSQUARE: x = (ACC)((x > ACC(0)) - (x < ACC(0))) * x * x; break;
       case TI_TRANSFORM_LOG1PEXP: x = ti::t_log1p(ti::t_exp(x)); break;
+      case TI_TRANSFORM_STEP: x = x >= ACC(0) ? ACC(1) : ACC(0); break;
       default: break;
     }
     o[k] = x;

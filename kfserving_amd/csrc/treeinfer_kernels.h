@@ -308,6 +308,9 @@ __device__ __forceinline__ void finish_row(const ACC (&acc)[KMAX], const KArgs& 
       case TI_TRANSFORM_LOG1PEXP:
         v = t_log1p(t_exp(v));
         break;
+      case TI_TRANSFORM_STEP:
+        v = v >= ACC(0) ? ACC(1) : ACC(0);
+        break;
       default:
         break;
     }

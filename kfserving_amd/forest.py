@@ -37,6 +37,7 @@ T_HINGE = 4
 T_EXP = 5
 T_SIGNSQUARE = 6
 T_LOG1PEXP = 7
+T_STEP = 8          # x >= 0 -> 1 (sklearn binary GradientBoostingClassifier.predict)
 
 # output kinds
 OUT_MARGIN = 0

@@ -4,7 +4,7 @@ Replaces the estimator the reference unpickles at
 python/sklearnserver/sklearnserver/model.py:38 (``joblib.load``) and calls at
 :50 (``self._model.predict``).  Supported: DecisionTree{Regressor,Classifier},
 RandomForest{Regressor,Classifier}, ExtraTrees{Regressor,Classifier} with one
-output.
+output, and GradientBoosting{Regressor,Classifier} (forest_from_gradient_boosting).
 
 Predict semantics encoded (installed sklearn 1.7.2,
 sklearn/tree/_tree.pyx:979-997 and sklearn/ensemble/_forest.py:723-736,
@@ -20,7 +20,7 @@ from typing import Tuple
 
 import numpy as np
 
-from ..forest import (Forest, NODE_NAN_LEFT, TI_F32, TI_F64, T_ARGMAX, T_IDENTITY,
+from ..forest import (Forest, NODE_NAN_LEFT, TI_F32, TI_F64, T_ARGMAX, T_IDENTITY, T_STEP,
                       concat_trees)
 
 TREE_LEAF = -1
@@ -93,8 +93,66 @@ def _estimators(est) -> Tuple[list, bool]:
                     "(RandomForest / ExtraTrees / DecisionTree)")
 
 
+def forest_from_gradient_boosting(est) -> Forest:
+    """GradientBoosting{Regressor,Classifier} (installed sklearn 1.7.2,
+    ensemble/_gb.py:948-967 and _gradient_boosting.pyx:56-75, 164-205):
+
+        raw[:, k] = init_raw[k];  for stage i, for k: raw[:, k] += learning_rate * value[leaf]
+
+    in float64 with X converted to float32 and ``x <= threshold`` (NaN input is
+    rejected by validate_data).  Each stage's K trees are output groups 0..K-1
+    in stage order, and the leaf payload is ``learning_rate * value`` (the same
+    double product the Cython loop forms), so the sums are bit-identical.  The
+    init estimator must be 'zero' or a Dummy{Regressor,Classifier} (the
+    default): its raw prediction is a constant per output, taken from the
+    estimator itself.  predict: regressor raw; binary classifier raw >= 0
+    (_gb.py:1612-1632, T_STEP); multiclass first argmax."""
+    from sklearn.dummy import DummyClassifier, DummyRegressor
+    init = est.init_
+    if not (isinstance(init, str) and init == "zero") and \
+            not isinstance(init, (DummyRegressor, DummyClassifier)):
+        raise TypeError("GradientBoosting with a non-constant init estimator "
+                        f"({type(init).__name__}) is not supported")
+    stages = est.estimators_                       # [n_stages, K] DecisionTreeRegressor
+    n_stages, K = stages.shape
+    F = int(est.n_features_in_)
+    base = np.asarray(est._raw_predict_init(np.zeros((1, F), dtype=np.float32))[0],
+                      dtype=np.float64)
+    lr = float(est.learning_rate)
+    canon, groups = [], []
+    for i in range(n_stages):
+        for k in range(K):
+            arr = tree_arrays_from_sklearn(stages[i, k].tree_)
+            t = _canon_tree(arr, False, 1)
+            t["flags"] = np.zeros_like(t["flags"])      # the GB traversal ignores missing_go_to_left
+            leaf = t["feature"] < 0
+            t["leaf_value"] = np.where(leaf[:, None], lr * arr["value"][:, 0, :1], 0.0)
+            canon.append(t)
+            groups.append(k)
+    cat = concat_trees(canon, 1)
+    classifier = hasattr(est, "classes_")
+    if classifier:
+        transform = T_STEP if K == 1 else T_ARGMAX
+    else:
+        transform = T_IDENTITY
+    return Forest(
+        n_features=F, n_groups=K, leaf_width=1, accum_dtype=TI_F64,
+        base_first=True, lgb_zero_map=False,
+        tree_offset=cat["tree_offset"], tree_group=np.asarray(groups, dtype=np.int32),
+        feature=cat["feature"], threshold=cat["threshold"], flags=cat["flags"],
+        left=cat["left"], right=cat["right"], leaf_id=cat["leaf_id"],
+        leaf_value=cat["leaf_value"], base_margin=base, average_divisor=1.0,
+        transform=transform, transform_param=1.0,
+        input_dtype=TI_F32, library="sklearn", objective=type(est).__name__,
+        meta={"classes": np.asarray(est.classes_) if classifier else None,
+              "allow_nan": False},
+    ).contiguous()
+
+
 def forest_from_sklearn(est) -> Forest:
     """Flatten a fitted sklearn tree ensemble."""
+    if type(est).__name__ in ("GradientBoostingRegressor", "GradientBoostingClassifier"):
+        return forest_from_gradient_boosting(est)
     members, average = _estimators(est)
     if getattr(est, "n_outputs_", 1) != 1:
         raise ValueError("multi-output sklearn models are not supported")

@@ -60,6 +60,8 @@ class SKLearnModel(GPUForestMixin, KFModel):  # pylint:disable=c-extension-no-me
             if X.shape[1] != f.n_features:
                 raise ValueError("X has %d features, but %s is expecting %d features as input."
                                  % (X.shape[1], f.objective, f.n_features))
+            if not f.meta.get("allow_nan", True) and np.isnan(X).any():
+                raise ValueError("Input X contains NaN.")   # GradientBoosting: validate_data
             if np.isinf(X).any():
                 raise ValueError("Input X contains infinity or a value too large for "
                                  "dtype('float32').")

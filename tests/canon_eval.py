@@ -5,7 +5,7 @@ reproduces the oracle, independently of the GPU kernels."""
 import numpy as np
 
 from kfserving_amd.forest import (NODE_CATEGORICAL, NODE_NAN_LEFT, NODE_ZERO_FLIP, OUT_LEAF, OUT_MARGIN,
-                                  T_ARGMAX, T_EXP, T_HINGE, T_IDENTITY, T_SIGMOID, T_SOFTMAX,
+                                  T_ARGMAX, T_EXP, T_HINGE, T_IDENTITY, T_SIGMOID, T_SOFTMAX, T_STEP,
                                   TI_F32, round_down_f32)
 
 
@@ -86,6 +86,9 @@ def predict(f, X, kind=1):
         return p if K > 1 else p[:, 0]
     if f.transform == T_HINGE:
         p = np.where(m > 0, acc_t(1), acc_t(0))
+        return p if K > 1 else p[:, 0]
+    if f.transform == T_STEP:
+        p = np.where(m >= 0, acc_t(1), acc_t(0))
         return p if K > 1 else p[:, 0]
     if f.transform == T_EXP:
         p = np.exp(m)

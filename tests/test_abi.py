@@ -69,7 +69,7 @@ def test_abi_constants_match_python():
     assert (v("TI_OUTPUT_MARGIN"), v("TI_OUTPUT_PREDICT"), v("TI_OUTPUT_LEAF")) == \
         (F.OUT_MARGIN, F.OUT_PREDICT, F.OUT_LEAF)
     for name in ("IDENTITY", "SIGMOID", "SOFTMAX", "ARGMAX", "HINGE", "EXP", "SIGNSQUARE",
-                 "LOG1PEXP"):
+                 "LOG1PEXP", "STEP"):
         assert v("TI_TRANSFORM_" + name) == getattr(F, "T_" + name)
 
 

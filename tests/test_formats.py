@@ -211,3 +211,39 @@ def test_lgb_inputs_by_name():
 def test_malformed_xgb_rejected():
     with pytest.raises(ValueError):
         parse_xgboost_bytes(b"\x00" * 100)
+
+
+# ----------------------------------------------- sklearn GradientBoosting
+def _gb_models():
+    from sklearn.ensemble import GradientBoostingClassifier, GradientBoostingRegressor
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((600, 7)).astype(np.float32)
+    y = X[:, 0] * 2 + np.sin(X[:, 1]) + 0.1 * rng.standard_normal(600)
+    reg = GradientBoostingRegressor(n_estimators=25, max_depth=4, learning_rate=0.07,
+                                    random_state=0).fit(X, y)
+    binc = GradientBoostingClassifier(n_estimators=20, max_depth=3, random_state=0) \
+        .fit(X, (y > 0.3).astype(int))
+    mult = GradientBoostingClassifier(n_estimators=15, max_depth=3, random_state=0) \
+        .fit(X, np.digitize(y, [-1.0, 0.0, 1.5]))
+    zero = GradientBoostingRegressor(n_estimators=10, max_depth=3, init="zero",
+                                     random_state=0).fit(X, y)
+    return X, reg, binc, mult, zero
+
+
+def test_sklearn_gradient_boosting_restated_bit_exact():
+    """canonical forest (numpy evaluator) == sklearn's own decision_function / predict"""
+    from kfserving_amd.formats.sklearn_format import forest_from_sklearn
+    from kfserving_amd.forest import OUT_MARGIN, OUT_PREDICT
+    X, reg, binc, mult, zero = _gb_models()
+    Xt = np.random.default_rng(1).standard_normal((500, 7)).astype(np.float32)
+    Xt[:5] = X[:5]
+    for est in (reg, zero):
+        f = forest_from_sklearn(est)
+        assert np.array_equal(canon_eval.predict(f, Xt, OUT_PREDICT), est.predict(Xt))
+    for est in (binc, mult):
+        f = forest_from_sklearn(est)
+        raw = canon_eval.predict(f, Xt, OUT_MARGIN)
+        want = est.decision_function(Xt)
+        assert np.array_equal(raw.reshape(want.shape), want)
+        lab = f.meta["classes"].take(canon_eval.predict(f, Xt, OUT_PREDICT).astype(np.int64))
+        assert np.array_equal(lab, est.predict(Xt))

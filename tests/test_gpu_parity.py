@@ -439,3 +439,31 @@ def test_bexplicit_zero_missing_and_specials(rows):
     X32 = X.astype(np.float32)
     assert np.array_equal(dev.predict(X32, OUT_MARGIN),
                           port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
+
+
+# ------------------------------------------------- sklearn GradientBoosting
+def test_sklearn_gradient_boosting_gpu_bit_exact(tmp_path):
+    from tests.test_formats import _gb_models
+    from kfserving_amd.formats.sklearn_format import forest_from_sklearn
+    X, reg, binc, mult, zero = _gb_models()
+    Xt = np.random.default_rng(2).standard_normal((3000, 7)).astype(np.float32)
+    for est in (reg, zero):
+        dev = DeviceForest(forest_from_sklearn(est), [0])
+        assert np.array_equal(dev.predict(Xt, OUT_PREDICT), est.predict(Xt))
+    for est in (binc, mult):
+        f = forest_from_sklearn(est)
+        dev = DeviceForest(f, [0])
+        want = est.decision_function(Xt)
+        assert np.array_equal(dev.predict(Xt, OUT_MARGIN).reshape(want.shape), want)
+        lab = f.meta["classes"].take(dev.predict(Xt, OUT_PREDICT).astype(np.int64))
+        assert np.array_equal(lab, est.predict(Xt))
+    # through the sklearnserver plugin, loading a joblib file as the reference does
+    import joblib
+    from kfserving_amd.sklearnserver import SKLearnModel
+    joblib.dump(mult, str(tmp_path / "model.joblib"))
+    model = SKLearnModel("gb", str(tmp_path))
+    assert model.load()
+    got = model.predict({"instances": Xt[:64].tolist()})["predictions"]
+    assert got == est.predict(Xt[:64]).tolist()
+    with pytest.raises(Exception, match="NaN"):
+        model.predict({"instances": [[float("nan")] * 7]})
