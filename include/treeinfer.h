@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define TI_ABI_VERSION 2
+#define TI_ABI_VERSION 3
 
 /* return codes */
 #define TI_OK               0
@@ -99,6 +99,9 @@ extern "C" {
 #define TI_OUTPUT_MARGIN   0  /* raw score (after base/average), [rows, K]     */
 #define TI_OUTPUT_PREDICT  1  /* transformed score, [rows, K] or [rows]       */
 #define TI_OUTPUT_LEAF     2  /* library leaf id per tree (int32), [rows, T]   */
+#define TI_OUTPUT_CONTRIB  3  /* TreeSHAP contributions, [rows, K * (F + 1)]:  */
+                              /* per group F feature columns, then the bias     */
+                              /* (xgboost pred_contribs); needs desc.cover      */
 
 /*
  * Canonical forest: host structure-of-arrays over the nodes of all trees,
@@ -137,6 +140,11 @@ typedef struct ti_forest_desc {
   const uint32_t* cat_bits;   /* [W]   bitset words of all categorical nodes        */
   const int64_t* cat_offset;  /* [N]   first word of node n's bitset                */
   const int32_t* cat_nwords;  /* [N]   words in node n's bitset                     */
+  /* node covers (ABI 3): the child weights of TreeSHAP (xgboost sum_hess,
+   * LightGBM internal/leaf counts, sklearn weighted_n_node_samples); NULL when
+   * the model file has none -- TI_OUTPUT_CONTRIB is then unsupported.  Replaces
+   * XGBoosterPredict(option_mask = pred_contribs) / LGBM predict_type = 3. */
+  const double*  cover;       /* [N]                                                */
 } ti_forest_desc;
 
 typedef struct ti_forest ti_forest;   /* opaque, owns device memory */

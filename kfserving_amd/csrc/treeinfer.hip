@@ -36,6 +36,109 @@ using ti::ExpNode;
 using ti::HeapNode;
 using ti::KArgs;
 
+// ---------------------------------------------------------- TreeSHAP paths
+// Every root-to-leaf path of every tree, with the splits on one feature
+// merged into one element (the unique path xgboost's TreeShap keeps: a
+// feature seen again is unwound and re-extended at the end, so elements are
+// in order of last occurrence).  An element holds the product of the
+// child/parent cover ratios of its splits (zero fraction) and the condition
+// a row must meet to follow all of them (one fraction 1, else 0).
+struct ShapPath {
+  int32_t group;    // output group (leaf_width 1)
+  int32_t n;        // elements (excluding the root's dummy element)
+  int64_t first;    // first element
+  int64_t leaf;     // row of the path's leaf in the leaf-value table
+};
+constexpr uint32_t kShapNanOk = 1u;    // NaN follows every split of the element
+constexpr uint32_t kShapZeroOk = 2u;   // exact 0 follows every split (LightGBM zero rule)
+constexpr uint32_t kShapEmpty = 4u;    // no non-NaN value follows (a left turn at a NaN threshold)
+struct ShapElem {
+  int32_t feature;
+  uint32_t flags;
+  double lo;        // follows iff lo < x <= hi (non-NaN, non-zero x)
+  double hi;
+  double zf;        // zero fraction
+};
+
+// One row per lane (64-row blocks).  Per path: the one fractions of the
+// row, then the path weights extended from scratch (ExtendPath) and, per
+// element, the unwound sum (UnwoundPathSum) times (one - zero) times the
+// leaf value, added to the element's feature.  Path weights and one
+// fractions live in LDS as [index][lane].  acc is float64 [rows, K*(F+1)];
+// the last pass divides by average_divisor, writes the bias and converts to
+// ACC.
+template <typename XT, typename ACC>
+__global__ void __launch_bounds__(64) contrib_kernel(
+    const XT* __restrict__ X, int64_t rows, int64_t stride, int32_t cols, int32_t zero_map_on,
+    const ShapPath* __restrict__ paths, int64_t n_paths, const ShapElem* __restrict__ elems,
+    const double* __restrict__ leafv, int32_t LW, int32_t K, int32_t F, int32_t maxl,
+    const double* __restrict__ bias, double divisor, double* __restrict__ acc,
+    ACC* __restrict__ out) {
+  extern __shared__ double shap_lds[];
+  const int lane = threadIdx.x;
+  const int64_t row = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = row < rows;
+  double* w = shap_lds;                         // [maxl + 1][64]
+  double* ob = shap_lds + (size_t)(maxl + 1) * 64;   // [maxl][64]
+  const XT* xr = X + (live ? row : rows - 1) * stride;
+  const int W = K * (F + 1);
+  double* ph = acc + (live ? row : 0) * W;
+  for (int64_t p = 0; p < n_paths; ++p) {
+    const ShapPath P = paths[p];
+    const int n = P.n;
+    for (int i = 0; i < n; ++i) {
+      const ShapElem e = elems[P.first + i];
+      double x = e.feature < cols ? (double)xr[e.feature] : __builtin_nan("");
+      if (zero_map_on && __builtin_fabs(x) <= (double)1e-35f) x = 0.0;
+      bool follow;
+      if (x != x) follow = (e.flags & kShapNanOk) != 0;
+      else if (x == 0.0) follow = (e.flags & kShapZeroOk) != 0;
+      else follow = !(e.flags & kShapEmpty) && e.lo < x && x <= e.hi;
+      ob[i * 64 + lane] = follow ? 1.0 : 0.0;
+    }
+    w[lane] = 1.0;
+    for (int d = 1; d <= n; ++d) {
+      const double zf = elems[P.first + d - 1].zf;
+      const double of = ob[(d - 1) * 64 + lane];
+      w[d * 64 + lane] = 0.0;
+      for (int i = d - 1; i >= 0; --i) {
+        w[(i + 1) * 64 + lane] += of * w[i * 64 + lane] * (i + 1) / (double)(d + 1);
+        w[i * 64 + lane] = zf * w[i * 64 + lane] * (d - i) / (double)(d + 1);
+      }
+    }
+    for (int e_i = 1; e_i <= n; ++e_i) {
+      const ShapElem e = elems[P.first + e_i - 1];
+      const double of = ob[(e_i - 1) * 64 + lane];
+      const double zf = e.zf;
+      double next = w[n * 64 + lane];
+      double total = 0.0;
+      for (int i = n - 1; i >= 0; --i) {
+        if (of != 0.0) {
+          const double tmp = next * (n + 1) / ((i + 1) * of);
+          total += tmp;
+          next = w[i * 64 + lane] - tmp * zf * (n - i) / (double)(n + 1);
+        } else {
+          total += (w[i * 64 + lane] / zf) / ((n - i) / (double)(n + 1));
+        }
+      }
+      const double scale = total * (of - zf);
+      if (live) {
+        if (LW == 1) {
+          ph[P.group * (F + 1) + e.feature] += scale * leafv[P.leaf];
+        } else {
+          for (int k = 0; k < LW; ++k) ph[k * (F + 1) + e.feature] += scale * leafv[P.leaf * LW + k];
+        }
+      }
+    }
+  }
+  if (!live) return;
+  ACC* o = out + row * W;
+  for (int g = 0; g < K; ++g) {
+    for (int f = 0; f < F; ++f) o[g * (F + 1) + f] = (ACC)(ph[g * (F + 1) + f] / divisor);
+    o[g * (F + 1) + F] = (ACC)bias[g];
+  }
+}
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -125,6 +228,11 @@ struct DeviceForest {
   // binned explicit layout: rank-coded nodes + tables per input dtype
   ExpNode* bx_nodes[2] = {nullptr, nullptr};
   unsigned char* bx_tbl[2] = {nullptr, nullptr};
+  // TreeSHAP path tables
+  ShapPath* shap_paths = nullptr;
+  ShapElem* shap_elems = nullptr;
+  double* shap_leaf = nullptr;
+  double* shap_bias = nullptr;
   // ti_predict scratch: device buffers + pinned host staging (grown x2)
   void* x_buf = nullptr;
   size_t x_cap = 0;
@@ -186,6 +294,12 @@ struct ti_forest {
   } bx[2];
   int32_t bx_ilp = 4;               // trees per lane in lockstep (4 or 8)
   std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
+  // TreeSHAP (TI_OUTPUT_CONTRIB); has_shap = 0 when the forest has no covers
+  int32_t has_shap = 0, shap_maxl = 0;
+  int64_t shap_npaths = 0;
+  std::vector<ShapPath> h_paths;
+  std::vector<ShapElem> h_elems;
+  std::vector<double> h_path_leaf, h_shap_bias;
   // host images (kept until upload)
   std::vector<unsigned char> h_heap32, h_heap64;
   std::vector<int32_t> h_heap_leaf_ids;
@@ -220,7 +334,8 @@ void free_device(DeviceForest& d) {
                   d.cpt_img[0], d.cpt_img[1], d.cpt_off[0], d.cpt_off[1], d.cpt_stage[0],
                   d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root, d.cat_words,
                   d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1],
-                  d.bx_nodes[0], d.bx_nodes[1], d.bx_tbl[0], d.bx_tbl[1]};
+                  d.bx_nodes[0], d.bx_nodes[1], d.bx_tbl[0], d.bx_tbl[1],
+                  d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d.hx_pin) (void)hipHostFree(d.hx_pin);
@@ -245,6 +360,9 @@ void free_device(DeviceForest& d) {
     d.bh_img[i] = d.bh_tbl[i] = d.bx_tbl[i] = nullptr;
     d.bx_nodes[i] = nullptr;
   }
+  d.shap_paths = nullptr;
+  d.shap_elems = nullptr;
+  d.shap_leaf = d.shap_bias = nullptr;
   d.x_cap = d.out_cap = 0;
   d.stream = nullptr;
   d.device = -1;
@@ -733,12 +851,111 @@ bool pack_bexplicit(const ti_forest_desc* d, ti_forest* f, ti_forest::BinExplici
   return true;
 }
 
+// TreeSHAP path tables + bias (see ShapPath).  Forests without covers or
+// with categorical splits get none (TI_OUTPUT_CONTRIB is then unsupported).
+struct ShapBuilder {
+  const ti_forest_desc* d;
+  ti_forest* f;
+  int64_t b = 0;
+  int group = 0;
+  std::vector<ShapElem> cur;
+
+  void dfs(int32_t v) {
+    const int64_t g = b + v;
+    const int LW = d->leaf_width;
+    if (d->feature[g] < 0) {
+      ShapPath p;
+      p.group = group;
+      p.n = static_cast<int32_t>(cur.size());
+      p.first = static_cast<int64_t>(f->h_elems.size());
+      p.leaf = static_cast<int64_t>(f->h_path_leaf.size()) / LW;
+      f->h_elems.insert(f->h_elems.end(), cur.begin(), cur.end());
+      for (int k = 0; k < LW; ++k) f->h_path_leaf.push_back(d->leaf_value[g * LW + k]);
+      f->h_paths.push_back(p);
+      f->shap_maxl = std::max(f->shap_maxl, p.n);
+      return;
+    }
+    const int32_t fe = d->feature[g];
+    const double t = d->threshold[g];
+    const bool nan_left = (d->flags[g] & TI_NODE_NAN_LEFT) != 0;
+    const bool zero_left = (d->flags[g] & TI_NODE_ZERO_FLIP) ? !(0 <= t) : (0 <= t);
+    for (int side = 0; side < 2; ++side) {
+      const bool left = side == 0;
+      const int32_t child = left ? d->left[g] : d->right[g];
+      const std::vector<ShapElem> saved = cur;
+      ShapElem e{fe, kShapNanOk | kShapZeroOk, -INFINITY, INFINITY, 1.0};
+      for (size_t i = 0; i < cur.size(); ++i)
+        if (cur[i].feature == fe) {   // unwind the earlier split on fe, re-extend at the end
+          e = cur[i];
+          cur.erase(cur.begin() + static_cast<std::ptrdiff_t>(i));
+          break;
+        }
+      e.zf = (d->cover[b + child] / d->cover[g]) * e.zf;
+      if (left) {
+        if (std::isnan(t)) e.flags |= kShapEmpty;
+        else e.hi = std::min(e.hi, t);
+      } else if (!std::isnan(t)) {
+        e.lo = std::max(e.lo, t);
+      }
+      if (nan_left != left) e.flags &= ~kShapNanOk;
+      if (zero_left != left) e.flags &= ~kShapZeroOk;
+      cur.push_back(e);
+      dfs(child);
+      cur = saved;
+    }
+  }
+
+  std::vector<double> mean(int32_t v) {   // FillNodeMeanValues, per leaf-vector entry
+    const int64_t g = b + v;
+    const int LW = d->leaf_width;
+    std::vector<double> r(LW);
+    if (d->feature[g] < 0) {
+      for (int k = 0; k < LW; ++k) r[k] = d->leaf_value[g * LW + k];
+      return r;
+    }
+    const int32_t l = d->left[g], rr = d->right[g];
+    const std::vector<double> ml = mean(l), mr = mean(rr);
+    for (int k = 0; k < LW; ++k)
+      r[k] = (ml[k] * d->cover[b + l] + mr[k] * d->cover[b + rr]) / d->cover[g];
+    return r;
+  }
+};
+
+void build_shap(const ti_forest_desc* d, ti_forest* f) {
+  if (!d->cover) return;
+  for (int64_t g = 0; g < d->n_nodes; ++g)
+    if (d->feature[g] >= 0 && (d->flags[g] & TI_NODE_CATEGORICAL)) return;
+  const int K = d->n_groups;
+  std::vector<double> bias(K);
+  for (int k = 0; k < K; ++k) bias[k] = d->base_margin[k] * d->average_divisor;
+  ShapBuilder sb{d, f};
+  for (int t = 0; t < d->n_trees; ++t) {
+    sb.b = d->tree_offset[t];
+    sb.group = d->leaf_width == 1 ? d->tree_group[t] : 0;
+    sb.cur.clear();
+    sb.dfs(0);
+    const std::vector<double> m = sb.mean(0);
+    if (d->leaf_width == 1) bias[sb.group] += m[0];
+    else for (int k = 0; k < K; ++k) bias[k] += m[k];
+  }
+  f->h_shap_bias.resize(K);
+  for (int k = 0; k < K; ++k) f->h_shap_bias[k] = bias[k] / d->average_divisor;
+  f->shap_npaths = static_cast<int64_t>(f->h_paths.size());
+  f->has_shap = 1;
+}
+
 int upload_device(ti_forest* f, DeviceForest& d, int device) {
   d.device = device;
   TI_HIP(hipSetDevice(device));
   TI_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   int rc;
   if ((rc = upload(&d.tree_group, f->h_group, &d.bytes))) return rc;
+  if (f->has_shap) {
+    if ((rc = upload(&d.shap_paths, f->h_paths, &d.bytes))) return rc;
+    if ((rc = upload(&d.shap_elems, f->h_elems, &d.bytes))) return rc;
+    if ((rc = upload(&d.shap_leaf, f->h_path_leaf, &d.bytes))) return rc;
+    if ((rc = upload(&d.shap_bias, f->h_shap_bias, &d.bytes))) return rc;
+  }
   if (f->layout == 0) {
     if ((rc = upload(&d.heap32, f->h_heap32, &d.bytes))) return rc;
     if ((rc = upload(&d.heap64, f->h_heap64, &d.bytes))) return rc;
@@ -836,6 +1053,7 @@ int ensure_lds_attr(int device, KernelFn fn) {
 
 int64_t output_width(const ti_forest* f, int kind) {
   if (kind == TI_OUTPUT_LEAF) return f->T;
+  if (kind == TI_OUTPUT_CONTRIB) return static_cast<int64_t>(f->K) * (f->F + 1);
   if (kind == TI_OUTPUT_PREDICT && f->transform == TI_TRANSFORM_ARGMAX) return 1;
   return f->K;
 }
@@ -1145,9 +1363,10 @@ int launch_chunked(ti_forest* f, int slot, const void* X, int xdt, int64_t rows,
   int32_t* dmap = nullptr;
   int rc = TI_OK;
   size_t tmp_bytes = 0;
+  const int64_t cw = kind == TI_OUTPUT_CONTRIB ? f->F + 1 : 1;   // columns per group
   for (auto& p : f->parts)
     tmp_bytes = std::max(tmp_bytes, static_cast<size_t>(rows) *
-                                        (kind == TI_OUTPUT_LEAF ? 4 * p->T : as * p->K));
+                                        (kind == TI_OUTPUT_LEAF ? 4 * p->T : as * p->K * cw));
   TI_HIP(hipMallocAsync(&tmp, tmp_bytes, stream));
   const bool transform = kind == TI_OUTPUT_PREDICT && f->transform != TI_TRANSFORM_IDENTITY;
   if (transform) {
@@ -1176,10 +1395,12 @@ int launch_chunked(ti_forest* f, int slot, const void* X, int xdt, int64_t rows,
       (void)hipFreeAsync(dmap, stream);
       dmap = nullptr;
     } else {
-      rc = launch_any(p, slot, X, xdt, rows, cols, stride, TI_OUTPUT_MARGIN, tmp, stream);
+      const int pk = kind == TI_OUTPUT_CONTRIB ? TI_OUTPUT_CONTRIB : TI_OUTPUT_MARGIN;
+      rc = launch_any(p, slot, X, xdt, rows, cols, stride, pk, tmp, stream);
       if (rc) break;
-      if (hipMemcpy2DAsync(static_cast<unsigned char*>(mdst) + f->part_k0[c] * as, f->K * as, tmp,
-                           p->K * as, p->K * as, rows, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+      if (hipMemcpy2DAsync(static_cast<unsigned char*>(mdst) + f->part_k0[c] * cw * as,
+                           f->K * cw * as, tmp, p->K * cw * as, p->K * cw * as, rows,
+                           hipMemcpyDeviceToDevice, stream) != hipSuccess)
         rc = fail(TI_ERR_DEVICE, "margin column copy failed");
     }
   }
@@ -1200,8 +1421,65 @@ int launch_chunked(ti_forest* f, int slot, const void* X, int xdt, int64_t rows,
   return rc;
 }
 
+// TI_OUTPUT_CONTRIB on one (unchunked) forest: contrib_kernel over the
+// forest's path tables; float32 forests accumulate in a float64 scratch.
+int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows,
+                   int32_t cols, int64_t stride, void* out, hipStream_t stream) {
+  if (!f->has_shap)
+    return fail(TI_ERR_UNSUPPORTED,
+                "contributions need node covers (ti_forest_desc.cover) and no categorical splits");
+  const int64_t W = static_cast<int64_t>(f->K) * (f->F + 1);
+  double* acc = nullptr;
+  if (f->accum == TI_F64) {
+    acc = static_cast<double*>(out);
+  } else {
+    TI_HIP(hipMallocAsync(reinterpret_cast<void**>(&acc), static_cast<size_t>(rows * W) * 8, stream));
+  }
+  TI_HIP(hipMemsetAsync(acc, 0, static_cast<size_t>(rows * W) * 8, stream));
+  const size_t lds = static_cast<size_t>(2 * f->shap_maxl + 1) * 64 * 8;
+  const int64_t n_paths = static_cast<int64_t>(d.shap_paths ? 1 : 0) * f->shap_npaths;
+  KernelFn fn;
+  if (xdt == TI_F32)
+    fn = f->accum == TI_F64 ? reinterpret_cast<KernelFn>(contrib_kernel<float, double>)
+                            : reinterpret_cast<KernelFn>(contrib_kernel<float, float>);
+  else
+    fn = f->accum == TI_F64 ? reinterpret_cast<KernelFn>(contrib_kernel<double, double>)
+                            : reinterpret_cast<KernelFn>(contrib_kernel<double, float>);
+  int rc = ensure_lds_attr(d.device, fn);
+  if (rc) return rc;
+  const unsigned grid = static_cast<unsigned>((rows + 63) / 64);
+  if (xdt == TI_F32) {
+    if (f->accum == TI_F64)
+      hipLaunchKernelGGL((contrib_kernel<float, double>), dim3(grid), dim3(64), lds, stream,
+                         static_cast<const float*>(X), rows, stride, cols, f->lgb_zero_map,
+                         d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,
+                         f->shap_maxl, d.shap_bias, f->divisor, acc, static_cast<double*>(out));
+    else
+      hipLaunchKernelGGL((contrib_kernel<float, float>), dim3(grid), dim3(64), lds, stream,
+                         static_cast<const float*>(X), rows, stride, cols, f->lgb_zero_map,
+                         d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,
+                         f->shap_maxl, d.shap_bias, f->divisor, acc, static_cast<float*>(out));
+  } else {
+    if (f->accum == TI_F64)
+      hipLaunchKernelGGL((contrib_kernel<double, double>), dim3(grid), dim3(64), lds, stream,
+                         static_cast<const double*>(X), rows, stride, cols, f->lgb_zero_map,
+                         d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,
+                         f->shap_maxl, d.shap_bias, f->divisor, acc, static_cast<double*>(out));
+    else
+      hipLaunchKernelGGL((contrib_kernel<double, float>), dim3(grid), dim3(64), lds, stream,
+                         static_cast<const double*>(X), rows, stride, cols, f->lgb_zero_map,
+                         d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,
+                         f->shap_maxl, d.shap_bias, f->divisor, acc, static_cast<float*>(out));
+  }
+  TI_HIP(hipGetLastError());
+  if (acc != out) TI_HIP(hipFreeAsync(acc, stream));
+  return TI_OK;
+}
+
 int launch_any(ti_forest* f, int slot, const void* X, int xdt, int64_t rows, int32_t cols,
                int64_t stride, int kind, void* out, hipStream_t stream) {
+  if (kind == TI_OUTPUT_CONTRIB && f->parts.empty())
+    return launch_contrib(f, *f->devs[slot], X, xdt, rows, cols, stride, out, stream);
   if (!f->parts.empty())
     return launch_chunked(f, slot, X, xdt, rows, cols, stride, kind, out, stream);
   return launch(f, *f->devs[slot], X, xdt, rows, cols, stride, kind, out, stream);
@@ -1229,7 +1507,7 @@ int create_chunked(const ti_forest_desc* d, const int32_t* devices, int32_t n_de
     const int kc = std::min(ti::kMaxGroups, K - k0);
     std::vector<int32_t> trees, tgrp, feat, left, right, leaf_id, cat_nw;
     std::vector<int64_t> toff(1, 0), cat_off;
-    std::vector<double> thr, lv, base(d->base_margin + k0, d->base_margin + k0 + kc);
+    std::vector<double> thr, lv, cov, base(d->base_margin + k0, d->base_margin + k0 + kc);
     std::vector<uint8_t> flags;
     for (int t = 0; t < d->n_trees; ++t) {
       if (LW == 1 && (d->tree_group[t] < k0 || d->tree_group[t] >= k0 + kc)) continue;
@@ -1242,6 +1520,7 @@ int create_chunked(const ti_forest_desc* d, const int32_t* devices, int32_t n_de
         left.push_back(d->left[g]);
         right.push_back(d->right[g]);
         leaf_id.push_back(d->leaf_id[g]);
+        if (d->cover) cov.push_back(d->cover[g]);
         if (d->cat_offset) {
           cat_off.push_back(d->cat_offset[g]);
           cat_nw.push_back(d->cat_nwords[g]);
@@ -1276,6 +1555,7 @@ int create_chunked(const ti_forest_desc* d, const int32_t* devices, int32_t n_de
     sd.transform_param = 1.0;
     sd.cat_offset = d->cat_offset ? cat_off.data() : nullptr;
     sd.cat_nwords = d->cat_offset ? cat_nw.data() : nullptr;
+    sd.cover = d->cover ? cov.data() : nullptr;
     ti_forest* part = nullptr;
     const int rc = ti_forest_create(&sd, devices, n_devices, &part);
     if (rc) {
@@ -1470,6 +1750,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
       }
     }
   }
+  build_shap(desc, f.get());
   for (int i = 0; i < n_devices; ++i) {
     f->devs.emplace_back(new DeviceForest());
     rc = upload_device(f.get(), *f->devs.back(), devices[i]);
@@ -1498,6 +1779,12 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   }
   f->h_exp_src.clear();
   f->h_exp_src.shrink_to_fit();
+  f->h_paths.clear();
+  f->h_paths.shrink_to_fit();
+  f->h_elems.clear();
+  f->h_elems.shrink_to_fit();
+  f->h_path_leaf.clear();
+  f->h_path_leaf.shrink_to_fit();
   for (auto& bi : f->bh) {
     bi.img.clear();
     bi.img.shrink_to_fit();
@@ -1539,7 +1826,7 @@ int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
 int ti_output_shape(const ti_forest* f, int32_t kind, int64_t n_rows, int64_t* out_len,
                     int32_t* out_dtype) {
   if (!f || !out_len || !out_dtype) return fail(TI_ERR_INVALID, "null argument");
-  if (kind < TI_OUTPUT_MARGIN || kind > TI_OUTPUT_LEAF) return fail(TI_ERR_INVALID, "bad output kind");
+  if (kind < TI_OUTPUT_MARGIN || kind > TI_OUTPUT_CONTRIB) return fail(TI_ERR_INVALID, "bad output kind");
   if (n_rows < 0) return fail(TI_ERR_INVALID, "negative n_rows");
   *out_len = n_rows * output_width(f, kind);
   *out_dtype = output_dtype(f, kind);
@@ -1550,7 +1837,7 @@ static int check_call(const ti_forest* f, const void* X, int32_t xdt, int64_t ro
                       int64_t stride, int32_t kind, const void* out, int64_t out_len) {
   if (!f) return fail(TI_ERR_INVALID, "null forest");
   if (xdt != TI_F32 && xdt != TI_F64) return fail(TI_ERR_INVALID, "x_dtype must be TI_F32 or TI_F64");
-  if (kind < TI_OUTPUT_MARGIN || kind > TI_OUTPUT_LEAF) return fail(TI_ERR_INVALID, "bad output kind");
+  if (kind < TI_OUTPUT_MARGIN || kind > TI_OUTPUT_CONTRIB) return fail(TI_ERR_INVALID, "bad output kind");
   if (rows < 0) return fail(TI_ERR_INVALID, "negative n_rows");
   if (rows == 0) return TI_OK;
   if (!X || !out) return fail(TI_ERR_INVALID, "null data pointer");

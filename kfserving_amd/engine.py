@@ -18,9 +18,10 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from .forest import (Forest, OUT_LEAF, OUT_MARGIN, OUT_PREDICT, TI_F32, TI_F64, TI_I32)
+from .forest import (Forest, OUT_CONTRIB, OUT_LEAF, OUT_MARGIN, OUT_PREDICT, TI_F32, TI_F64,
+                     TI_I32)
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("TREEINFER_LIB", os.path.join(_LIB_DIR, "libtreeinfer.so"))
 
@@ -67,6 +68,7 @@ class _ForestDesc(ctypes.Structure):
         ("cat_bits", ctypes.c_void_p),
         ("cat_offset", ctypes.c_void_p),
         ("cat_nwords", ctypes.c_void_p),
+        ("cover", ctypes.c_void_p),
     ]
 
 
@@ -191,6 +193,8 @@ class DeviceForest:
             desc.cat_bits = _ptr(f.cat_bits) if f.cat_bits.size else None
             desc.cat_offset = _ptr(f.cat_offset)
             desc.cat_nwords = _ptr(f.cat_nwords)
+        if f.cover is not None:
+            desc.cover = _ptr(f.cover)
         dev_arr = (ctypes.c_int32 * len(devs))(*devs)
         handle = ctypes.c_void_p()
         _check(self._lib, self._lib.ti_forest_create(ctypes.byref(desc), dev_arr, len(devs),
@@ -260,5 +264,5 @@ class DeviceForest:
 
 
 __all__ = ["DeviceForest", "TreeInferError", "load_library", "device_count", "default_devices",
-           "EXPORTED_SYMBOLS", "OUT_MARGIN", "OUT_PREDICT", "OUT_LEAF", "TI_F32", "TI_F64",
+           "EXPORTED_SYMBOLS", "OUT_MARGIN", "OUT_PREDICT", "OUT_LEAF", "OUT_CONTRIB", "TI_F32", "TI_F64",
            "TI_I32"]

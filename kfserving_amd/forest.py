@@ -43,6 +43,7 @@ T_STEP = 8          # x >= 0 -> 1 (sklearn binary GradientBoostingClassifier.pre
 OUT_MARGIN = 0
 OUT_PREDICT = 1
 OUT_LEAF = 2
+OUT_CONTRIB = 3     # TreeSHAP contributions [rows, K * (F + 1)], bias last per group
 
 # LightGBM missing types (decision_type bits 2-3)
 MISSING_NONE = 0
@@ -88,6 +89,9 @@ class Forest:
     cat_bits: Optional[np.ndarray] = None       # uint32 [W]
     cat_offset: Optional[np.ndarray] = None     # int64 [N]
     cat_nwords: Optional[np.ndarray] = None     # int32 [N]
+    # node covers (xgboost sum_hess, LightGBM data counts, sklearn weighted
+    # samples): the node weights of TreeSHAP contributions (OUT_CONTRIB)
+    cover: Optional[np.ndarray] = None          # float64 [N]
     library: str = ""
     objective: str = ""
     feature_names: Optional[List[str]] = None
@@ -147,6 +151,8 @@ class Forest:
         internal = self.feature >= 0
         if np.any(self.feature[internal] >= self.n_features):
             raise ValueError("split feature index >= n_features")
+        if self.cover is not None and self.cover.shape[0] != N:
+            raise ValueError("cover must be [n_nodes]")
         cat = internal & ((self.flags & NODE_CATEGORICAL) != 0)
         if cat.any():
             if self.cat_bits is None or self.cat_offset is None or self.cat_nwords is None:
@@ -168,6 +174,8 @@ class Forest:
         self.leaf_value = np.ascontiguousarray(
             np.asarray(self.leaf_value, dtype=np.float64).reshape(self.n_nodes, self.leaf_width))
         self.base_margin = np.ascontiguousarray(self.base_margin, dtype=np.float64)
+        if self.cover is not None:
+            self.cover = np.ascontiguousarray(self.cover, dtype=np.float64)
         if self.cat_bits is not None:
             self.cat_bits = np.ascontiguousarray(self.cat_bits, dtype=np.uint32)
             self.cat_offset = np.ascontiguousarray(self.cat_offset, dtype=np.int64)
@@ -181,6 +189,8 @@ class Forest:
     def output_width(self, kind: int) -> int:
         if kind == OUT_LEAF:
             return self.n_trees
+        if kind == OUT_CONTRIB:
+            return self.n_groups * (self.n_features + 1)
         if kind == OUT_PREDICT and self.transform == T_ARGMAX:
             return 1
         return self.n_groups
@@ -206,6 +216,10 @@ def concat_trees(trees: List[dict], leaf_width: int) -> Dict[str, np.ndarray]:
         cat[key] = np.concatenate([np.asarray(t[key], dtype=dt) for t in trees])
     cat["leaf_value"] = np.concatenate(
         [np.asarray(t["leaf_value"], dtype=np.float64).reshape(-1, leaf_width) for t in trees])
+    if all(t.get("cover") is not None for t in trees):
+        cat["cover"] = np.concatenate([np.asarray(t["cover"], dtype=np.float64) for t in trees])
+    else:
+        cat["cover"] = None
     cat["tree_offset"] = offset
     return cat
 

@@ -95,10 +95,12 @@ def _tree(block: Dict[str, str]) -> dict:
         raise LightGBMFormatError("leaf_value length != num_leaves")
     if block.get("is_linear", "0").strip() not in ("", "0"):
         raise LightGBMFormatError("linear trees are not supported")
+    leaf_count = _floats(block["leaf_count"]) if "leaf_count" in block else None
     if num_leaves == 1:
         return {"feature": np.array([-1]), "threshold": np.zeros(1), "flags": np.zeros(1),
                 "left": np.array([-1]), "right": np.array([-1]), "leaf_id": np.array([0]),
-                "leaf_value": leaf_value.reshape(1, 1)}
+                "leaf_value": leaf_value.reshape(1, 1),
+                "cover": None if leaf_count is None else leaf_count[:1]}
     n_int = num_leaves - 1
     feat = _ints(block["split_feature"])
     thr = _floats(block["threshold"])
@@ -134,6 +136,9 @@ def _tree(block: Dict[str, str]) -> dict:
         "leaf_id": np.concatenate([np.full(n_int, -1), np.arange(num_leaves)]),
         "leaf_value": np.concatenate([np.zeros(n_int), leaf_value]).reshape(n, 1),
         "cat_offset": cat_off, "cat_nwords": cat_nw, "cat_words": cat_words,
+        # data counts (LightGBM's own SHAP weights children by them)
+        "cover": (np.concatenate([_floats(block["internal_count"]), leaf_count])
+                  if leaf_count is not None and "internal_count" in block else None),
     }
 
 
@@ -200,7 +205,7 @@ def parse_lightgbm_text(text: str) -> Forest:
         tree_group=(np.arange(len(trees)) % K).astype(np.int32),
         feature=cat["feature"], threshold=cat["threshold"], flags=cat["flags"],
         left=cat["left"], right=cat["right"], leaf_id=cat["leaf_id"],
-        leaf_value=cat["leaf_value"], base_margin=np.zeros(K),
+        leaf_value=cat["leaf_value"], base_margin=np.zeros(K), cover=cat["cover"],
         average_divisor=float(n_iter) if average and n_iter > 0 else 1.0,
         transform=transform, transform_param=tparam, input_dtype=TI_F64,
         library="lightgbm", objective=objective, feature_names=names,
@@ -250,6 +255,10 @@ def write_lightgbm_text(path: str, trees: List[dict], n_features: int, objective
             out.append("cat_boundaries=" + " ".join(str(int(v)) for v in cb))
             out.append("cat_threshold=" + " ".join(str(int(v)) for v in t["cat_threshold"]))
         out.append("leaf_value=" + " ".join(_fmt(v) for v in t["leaf_value"]))
+        if "leaf_count" in t:
+            out.append("leaf_count=" + " ".join(str(int(v)) for v in t["leaf_count"]))
+            if nl > 1:
+                out.append("internal_count=" + " ".join(str(int(v)) for v in t["internal_count"]))
         out.append("shrinkage=1")
         out.append("")
         out.append("")
@@ -302,6 +311,7 @@ def synthetic_leafwise_trees(n_trees: int, num_leaves: int, n_features: int, see
     random current leaf until ``num_leaves``; thresholds ~ N(0,1) as float64,
     decision_type draws default_left and a missing type."""
     rng = np.random.default_rng(seed)
+    crng = np.random.default_rng([seed, 7919])
     trees = []
     mts = np.asarray(missing_types)
     for _ in range(n_trees):
@@ -328,7 +338,17 @@ def synthetic_leafwise_trees(n_trees: int, num_leaves: int, n_features: int, see
             leaf_owner.append((node, 1))
             left[node] = ~j
             right[node] = ~new_leaf
+        leaf_count = crng.integers(1, 200, size=num_leaves)   # own stream: trees unchanged
+        internal_count = np.zeros(n_int, dtype=np.int64)
+
+        def count(c):
+            if c < 0:
+                return int(leaf_count[~c])
+            internal_count[c] = count(int(left[c])) + count(int(right[c]))
+            return int(internal_count[c])
+        count(0)
         trees.append({"split_feature": feat, "threshold": thr, "decision_type": dtype_,
                       "left_child": left, "right_child": right,
-                      "leaf_value": rng.uniform(-0.05, 0.05, size=num_leaves)})
+                      "leaf_value": rng.uniform(-0.05, 0.05, size=num_leaves),
+                      "leaf_count": leaf_count, "internal_count": internal_count})
     return trees

@@ -38,6 +38,7 @@ def tree_arrays_from_sklearn(tree_) -> dict:
         "missing_go_to_left": (np.asarray(mgl, dtype=np.uint8) if mgl is not None
                                else np.zeros(n, dtype=np.uint8)),
         "value": np.asarray(tree_.value, dtype=np.float64),
+        "cover": np.asarray(tree_.weighted_n_node_samples, dtype=np.float64),
     }
 
 
@@ -58,6 +59,7 @@ def _canon_tree(arr: dict, classifier: bool, n_classes: int) -> dict:
         "right": np.where(leaf, -1, cr),
         "leaf_id": np.arange(n),
         "leaf_value": np.where(leaf[:, None], lv, 0.0),
+        "cover": arr.get("cover"),
     }
 
 
@@ -72,7 +74,7 @@ def forest_from_tree_arrays(trees, n_features: int, classifier: bool, n_classes:
         tree_offset=cat["tree_offset"], tree_group=np.zeros(len(trees), dtype=np.int32),
         feature=cat["feature"], threshold=cat["threshold"], flags=cat["flags"],
         left=cat["left"], right=cat["right"], leaf_id=cat["leaf_id"],
-        leaf_value=cat["leaf_value"], base_margin=np.zeros(K),
+        leaf_value=cat["leaf_value"], base_margin=np.zeros(K), cover=cat["cover"],
         average_divisor=float(len(trees)) if average else 1.0,
         transform=T_ARGMAX if classifier else T_IDENTITY, transform_param=1.0,
         input_dtype=TI_F32, library="sklearn", objective=kind,
@@ -141,7 +143,7 @@ def forest_from_gradient_boosting(est) -> Forest:
         tree_offset=cat["tree_offset"], tree_group=np.asarray(groups, dtype=np.int32),
         feature=cat["feature"], threshold=cat["threshold"], flags=cat["flags"],
         left=cat["left"], right=cat["right"], leaf_id=cat["leaf_id"],
-        leaf_value=cat["leaf_value"], base_margin=base, average_divisor=1.0,
+        leaf_value=cat["leaf_value"], base_margin=base, average_divisor=1.0, cover=cat["cover"],
         transform=transform, transform_param=1.0,
         input_dtype=TI_F32, library="sklearn", objective=type(est).__name__,
         meta={"classes": np.asarray(est.classes_) if classifier else None,
@@ -190,8 +192,8 @@ def load_tree_arrays(path: str) -> Forest:
     z = np.load(path, allow_pickle=False)
     T = int(z["n_trees"])
     keys = ("children_left", "children_right", "feature", "threshold", "missing_go_to_left",
-            "value")
-    trees = [{k: z[f"t{i}_{k}"] for k in keys} for i in range(T)]
+            "value", "cover")
+    trees = [{k: z[f"t{i}_{k}"] for k in keys if f"t{i}_{k}" in z.files} for i in range(T)]
     classifier = bool(int(z["classifier"]))
     return forest_from_tree_arrays(trees, int(z["n_features"]), classifier,
                                    int(z["n_classes"]), average=bool(int(z["average"])),

@@ -102,7 +102,11 @@ def xgb_threshold(split: np.ndarray) -> np.ndarray:
     return t
 
 
-def _tree_from_arrays(cleft, cright, sindex, value, deleted=None) -> dict:
+_STAT_DTYPE = np.dtype([("loss_chg", "<f4"), ("sum_hess", "<f4"), ("base_weight", "<f4"),
+                        ("leaf_child_cnt", "<i4")])
+
+
+def _tree_from_arrays(cleft, cright, sindex, value, deleted=None, sum_hess=None) -> dict:
     cleft = np.asarray(cleft, dtype=np.int32)
     cright = np.asarray(cright, dtype=np.int32)
     sindex = np.asarray(sindex, dtype=np.uint32)
@@ -123,6 +127,9 @@ def _tree_from_arrays(cleft, cright, sindex, value, deleted=None) -> dict:
         "right": np.where(leaf, -1, cright).astype(np.int32),
         "leaf_id": np.arange(n, dtype=np.int32),
         "leaf_value": np.where(leaf, value, np.float32(0)).astype(np.float64).reshape(n, 1),
+        # RTreeNodeStat::sum_hess, the cover TreeSHAP weights children by
+        "cover": None if sum_hess is None else np.asarray(sum_hess, dtype=np.float32)
+        .astype(np.float64),
     }
 
 
@@ -144,7 +151,7 @@ def _assemble(trees: List[dict], tree_info: np.ndarray, num_feature: int, num_gr
         tree_offset=cat["tree_offset"], tree_group=tinfo,
         feature=cat["feature"], threshold=cat["threshold"], flags=cat["flags"],
         left=cat["left"], right=cat["right"], leaf_id=cat["leaf_id"],
-        leaf_value=cat["leaf_value"], base_margin=base,
+        leaf_value=cat["leaf_value"], base_margin=base, cover=cat["cover"],
         transform=objective_transform(objective), transform_param=1.0,
         input_dtype=TI_F32, library="xgboost", objective=objective,
         feature_names=feature_names,
@@ -173,13 +180,13 @@ def _parse_binary(buf: bytes, pos: int, fmt: str) -> Forest:
         if num_nodes <= 0:
             raise XGBoostFormatError("tree with no nodes")
         nodes = np.frombuffer(r.take(_NODE_DTYPE.itemsize * num_nodes), dtype=_NODE_DTYPE)
-        r.take(_STAT_BYTES * num_nodes)
+        stats = np.frombuffer(r.take(_STAT_BYTES * num_nodes), dtype=_STAT_DTYPE)
         if t_slv != 0:
             (nlv,) = r.unpack("<Q")
             r.take(4 * nlv)
         deleted = nodes["sindex"] == _DELETED
         trees.append(_tree_from_arrays(nodes["cleft"], nodes["cright"], nodes["sindex"],
-                                       nodes["info"], deleted))
+                                       nodes["info"], deleted, stats["sum_hess"]))
     tree_info = np.frombuffer(r.take(4 * num_trees), dtype="<i4") if num_trees else np.zeros(0)
     if gbm == "dart":
         (nw,) = r.unpack("<Q")
@@ -236,7 +243,8 @@ def _parse_json(doc: dict) -> Forest:
         cleft = np.asarray(jt["left_children"], dtype=np.int32)
         dl = np.asarray(jt["default_left"], dtype=np.uint32) & 1
         sindex = np.asarray(jt["split_indices"], dtype=np.uint32) | (dl << 31)
-        t = _tree_from_arrays(cleft, jt["right_children"], sindex, jt["split_conditions"])
+        t = _tree_from_arrays(cleft, jt["right_children"], sindex, jt["split_conditions"],
+                              sum_hess=jt.get("sum_hessian"))
         if weights is not None:
             lv = t["leaf_value"][:, 0].astype(np.float32) * weights[i]
             t["leaf_value"] = lv.astype(np.float64).reshape(-1, 1)
@@ -318,7 +326,10 @@ def write_legacy_binary(path: str, trees: List[dict], tree_info, num_feature: in
                 parent[t["cright"][i]] = i
         nodes["parent"] = parent.astype(np.uint32).view(np.int32)
         out += nodes.tobytes()
-        out += bytes(_STAT_BYTES * n)
+        stats = np.zeros(n, dtype=_STAT_DTYPE)
+        if "sum_hess" in t:
+            stats["sum_hess"] = t["sum_hess"]
+        out += stats.tobytes()
     out += np.asarray(tree_info, dtype="<i4").tobytes()
     with open(path, "wb") as fh:
         fh.write(bytes(out))
@@ -340,6 +351,7 @@ def json_model_doc(trees: List[dict], tree_info, num_feature: int, num_class: in
             "split_indices": conv(np.asarray(t["sindex"]) & 0x7FFFFFFF, np.int32),
             "default_left": conv(np.asarray(t["sindex"]) >> 31, np.uint8),
             "split_conditions": conv(t["value"], np.float32),
+            "sum_hessian": conv(t.get("sum_hess", np.zeros(n)), np.float32),
             "tree_param": {"num_nodes": str(n), "num_feature": str(num_feature),
                            "size_leaf_vector": "0"},
         })
@@ -387,6 +399,7 @@ def synthetic_complete_trees(n_trees: int, depth: int, n_features: int, seed: in
     Bernoulli(1/2), leaf ~ U(-0.05, 0.05) float32; nodes numbered in heap order.
     """
     rng = np.random.default_rng(seed)
+    crng = np.random.default_rng([seed, 7919])   # covers: own stream, trees unchanged
     n_int = (1 << depth) - 1
     n = 2 * n_int + 1
     trees = []
@@ -403,7 +416,13 @@ def synthetic_complete_trees(n_trees: int, depth: int, n_features: int, seed: in
         value = np.zeros(n, dtype=np.float32)
         value[:n_int] = rng.standard_normal(n_int).astype(np.float32)
         value[n_int:] = rng.uniform(-0.05, 0.05, size=n - n_int).astype(np.float32)
-        trees.append({"cleft": cleft, "cright": cright, "sindex": sindex, "value": value})
+        # covers: leaf hessian sums ~ U(1, 100), a parent the float32 sum of its children
+        hess = np.zeros(n, dtype=np.float32)
+        hess[n_int:] = crng.uniform(1.0, 100.0, size=n - n_int).astype(np.float32)
+        for i in range(n_int - 1, -1, -1):
+            hess[i] = hess[2 * i + 1] + hess[2 * i + 2]
+        trees.append({"cleft": cleft, "cright": cright, "sindex": sindex, "value": value,
+                      "sum_hess": hess})
     K = max(1, num_class)
     tree_info = (np.arange(n_trees) % K).astype(np.int32)
     return trees, tree_info
@@ -412,7 +431,8 @@ def synthetic_complete_trees(n_trees: int, depth: int, n_features: int, seed: in
 def forest_from_raw_trees(trees: List[dict], tree_info, num_feature: int, num_class: int,
                           base_score: float, objective: str, legacy: bool = True) -> Forest:
     """Canonical forest straight from RegTree arrays (what the writers store)."""
-    canon = [_tree_from_arrays(t["cleft"], t["cright"], t["sindex"], t["value"]) for t in trees]
+    canon = [_tree_from_arrays(t["cleft"], t["cright"], t["sindex"], t["value"],
+                              sum_hess=t.get("sum_hess")) for t in trees]
     return _assemble(canon, tree_info, num_feature, max(1, num_class), base_score, objective,
                      base_is_margin=legacy, base_first=False,
                      version=(0, 82, 0) if legacy else (1, 3, 0), fmt="raw")

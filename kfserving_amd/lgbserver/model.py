@@ -8,6 +8,8 @@ reference called ``Booster.predict`` (:51).
 import os
 from typing import Dict
 
+import numpy as np
+
 from ..formats.lightgbm_format import load_lightgbm_model
 from ..forest import Forest
 from ..kfserving.kfmodel import KFModel
@@ -37,10 +39,12 @@ class LightGBMModel(GPUForestMixin, KFModel):
         names = self._forest.feature_names
         return list(names) if names else [f"Column_{j}" for j in range(self._forest.n_features)]
 
+    def request_matrix(self, request: Dict) -> np.ndarray:
+        return lgb_matrix_from_inputs(request["inputs"], self.feature_name())
+
     def predict(self, request: Dict) -> Dict:
         try:
-            X = lgb_matrix_from_inputs(request["inputs"], self.feature_name())
-            result = self.predict_matrix(X)
+            result = self.predict_matrix(self.request_matrix(request))
             return {"predictions": result.tolist()}
         except Exception as e:
             raise Exception("Failed to predict %s" % e)

@@ -45,27 +45,35 @@ class SKLearnModel(GPUForestMixin, KFModel):  # pylint:disable=c-extension-no-me
                 self.ready = True
         return self.ready
 
-    def predict(self, request: Dict) -> Dict:
+    def _array(self, request: Dict) -> np.ndarray:
         instances = request["instances"]
         try:
-            inputs = np.array(instances)
+            return np.array(instances)
         except Exception as e:
             raise Exception(
                 "Failed to initialize NumPy array from inputs: %s, %s" % (e, instances))
+
+    def request_matrix(self, request: Dict) -> np.ndarray:
+        """sklearn's validate_data checks on the ``instances`` array."""
+        f = self._forest
+        X = np.asarray(self._array(request), dtype=np.float64)
+        if X.ndim != 2:
+            raise ValueError("Expected 2D array, got %dD array instead" % X.ndim)
+        if X.shape[1] != f.n_features:
+            raise ValueError("X has %d features, but %s is expecting %d features as input."
+                             % (X.shape[1], f.objective, f.n_features))
+        if not f.meta.get("allow_nan", True) and np.isnan(X).any():
+            raise ValueError("Input X contains NaN.")   # GradientBoosting: validate_data
+        if np.isinf(X).any():
+            raise ValueError("Input X contains infinity or a value too large for "
+                             "dtype('float32').")
+        return X
+
+    def predict(self, request: Dict) -> Dict:
+        inputs = self._array(request)
         try:
             f = self._forest
-            X = np.asarray(inputs, dtype=np.float64)
-            if X.ndim != 2:
-                raise ValueError("Expected 2D array, got %dD array instead" % X.ndim)
-            if X.shape[1] != f.n_features:
-                raise ValueError("X has %d features, but %s is expecting %d features as input."
-                                 % (X.shape[1], f.objective, f.n_features))
-            if not f.meta.get("allow_nan", True) and np.isnan(X).any():
-                raise ValueError("Input X contains NaN.")   # GradientBoosting: validate_data
-            if np.isinf(X).any():
-                raise ValueError("Input X contains infinity or a value too large for "
-                                 "dtype('float32').")
-            result = self.predict_matrix(X)
+            result = self.predict_matrix(self.request_matrix({"instances": inputs}))
             classes = f.meta.get("classes")
             if classes is not None:
                 result = np.asarray(classes).take(result.astype(np.int64), axis=0)

@@ -10,12 +10,12 @@ library turns a JSON request into a feature matrix.
 from __future__ import annotations
 
 import threading
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
 from .engine import DeviceForest
-from .forest import OUT_PREDICT, Forest
+from .forest import OUT_CONTRIB, OUT_PREDICT, Forest
 
 
 class GPUForestMixin:
@@ -47,6 +47,25 @@ class GPUForestMixin:
 
     def predict_matrix(self, X: np.ndarray, kind: int = OUT_PREDICT) -> np.ndarray:
         return self.device_forest().predict(X, kind)
+
+    def explain(self, request: Dict) -> Dict:
+        """The ``:explain`` route (kfserver.py:79-82 in the reference, which
+        forwards to an explainer service; kfmodel.py:106-122) answered in
+        process: TreeSHAP feature contributions computed on the GPU
+        (libtreeinfer TI_OUTPUT_CONTRIB), shaped like xgboost's
+        ``predict(pred_contribs=True)``: [rows, F + 1] for one output group,
+        [rows, K, F + 1] for K groups; the last column is the bias (base
+        margin + expected tree output).  The request is parsed exactly as
+        ``predict`` parses it (``request_matrix``)."""
+        try:
+            X = self.request_matrix(request)
+            f = self._forest
+            c = self.predict_matrix(X, OUT_CONTRIB)
+            if f.n_groups > 1:
+                c = c.reshape(c.shape[0], f.n_groups, f.n_features + 1)
+            return {"explanations": c.tolist()}
+        except Exception as e:
+            raise Exception("Failed to explain %s" % e)
 
 
 def xgb_matrix_from_list(instances) -> np.ndarray:

@@ -36,14 +36,15 @@ class XGBoostModel(GPUForestMixin, KFModel):
         self.ready = True
         return self.ready
 
+    def request_matrix(self, request: Dict) -> np.ndarray:
+        instances = request["instances"]
+        if isinstance(instances, np.ndarray) and not isinstance(instances, JsonInstances):
+            return instances                      # DMatrix(ndarray): NaN = missing
+        return xgb_matrix_from_list(instances)    # DMatrix(list) semantics (JSON rows)
+
     def predict(self, request: Dict) -> Dict:
         try:
-            instances = request["instances"]
-            if isinstance(instances, np.ndarray) and not isinstance(instances, JsonInstances):
-                X = instances                      # DMatrix(ndarray): NaN = missing
-            else:
-                X = xgb_matrix_from_list(instances)   # DMatrix(list) semantics (JSON rows)
-            result = self.predict_matrix(X)
+            result = self.predict_matrix(self.request_matrix(request))
             return {"predictions": result.tolist()}
         except Exception as e:
             raise Exception("Failed to predict %s" % e)

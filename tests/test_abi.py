@@ -66,8 +66,8 @@ def test_abi_constants_match_python():
     assert (v("TI_F32"), v("TI_F64"), v("TI_I32")) == (F.TI_F32, F.TI_F64, F.TI_I32)
     assert (v("TI_NODE_NAN_LEFT"), v("TI_NODE_ZERO_FLIP"), v("TI_NODE_CATEGORICAL")) == \
         (F.NODE_NAN_LEFT, F.NODE_ZERO_FLIP, F.NODE_CATEGORICAL)
-    assert (v("TI_OUTPUT_MARGIN"), v("TI_OUTPUT_PREDICT"), v("TI_OUTPUT_LEAF")) == \
-        (F.OUT_MARGIN, F.OUT_PREDICT, F.OUT_LEAF)
+    assert (v("TI_OUTPUT_MARGIN"), v("TI_OUTPUT_PREDICT"), v("TI_OUTPUT_LEAF"),
+            v("TI_OUTPUT_CONTRIB")) == (F.OUT_MARGIN, F.OUT_PREDICT, F.OUT_LEAF, F.OUT_CONTRIB)
     for name in ("IDENTITY", "SIGMOID", "SOFTMAX", "ARGMAX", "HINGE", "EXP", "SIGNSQUARE",
                  "LOG1PEXP", "STEP"):
         assert v("TI_TRANSFORM_" + name) == getattr(F, "T_" + name)
@@ -86,3 +86,11 @@ def test_kfserve_library_exports_its_header():
     lib = fastjson.load_library()
     for n in names:
         assert hasattr(lib, n), n
+
+
+def test_plugin_modules_import():
+    """Every plugin module imports without a GPU (the device replica is lazy)."""
+    import importlib
+    for m in ("kfserving_amd.xgbserver.model", "kfserving_amd.lgbserver.model",
+              "kfserving_amd.sklearnserver.model", "kfserving_amd.tree_model"):
+        importlib.import_module(m)
