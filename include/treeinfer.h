@@ -199,6 +199,18 @@ int ti_predict_device(ti_forest* forest, int32_t device_slot, const void* X,
                       int64_t row_stride, int32_t output_kind, void* out,
                       int64_t out_len, void* hip_stream);
 
+/* The forest's output transform (TI_OUTPUT_PREDICT semantics) applied to
+ * margins summed elsewhere: in the tree-sharded mode each rank predicts
+ * TI_OUTPUT_MARGIN over its slice of the trees and the partial margins are
+ * summed by an RCCL reduce (kfserving_amd/tree_shard.py).  margin: [n_rows,
+ * n_groups] device array of the accumulation type (base margin included);
+ * out: ti_output_shape(TI_OUTPUT_PREDICT) elements on the same device, not
+ * aliasing margin.  Enqueued on hip_stream; returns without synchronising.
+ * Replaces the objective's PredTransform that XGBoosterPredict /
+ * LGBM_BoosterPredictForMat apply after summing the trees. */
+int ti_transform_device(ti_forest* forest, int32_t device_slot, const void* margin,
+                        int64_t n_rows, void* out, int64_t out_len, void* hip_stream);
+
 /* Thread-local message for the last failing call on this thread
  * (XGBGetLastError / LGBM_GetLastError). */
 const char* ti_last_error(void);

@@ -1880,6 +1880,34 @@ int ti_predict(ti_forest* f, const void* X, int32_t xdt, int64_t rows, int32_t c
   return TI_OK;
 }
 
+int ti_transform_device(ti_forest* f, int32_t slot, const void* margin, int64_t rows, void* out,
+                        int64_t out_len, void* stream) {
+  if (!f) return fail(TI_ERR_INVALID, "null forest");
+  if (rows < 0) return fail(TI_ERR_INVALID, "negative row count");
+  if (rows == 0) return TI_OK;
+  if (!margin || !out) return fail(TI_ERR_INVALID, "null margin or output");
+  if (margin == out) return fail(TI_ERR_INVALID, "margin and output must not alias");
+  if (out_len < rows * output_width(f, TI_OUTPUT_PREDICT))
+    return fail(TI_ERR_INVALID, "output buffer too small");
+  ti_forest* bf = base_forest(f);
+  if (slot < 0 || slot >= static_cast<int>(bf->devs.size()))
+    return fail(TI_ERR_INVALID, "device_slot out of range");
+  TI_HIP(hipSetDevice(bf->devs[slot]->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int threads = 256;
+  const unsigned grid = static_cast<unsigned>((rows + threads - 1) / threads);
+  if (f->accum == TI_F64)
+    hipLaunchKernelGGL(transform_rows_kernel<double>, dim3(grid), dim3(threads), 0, s,
+                       static_cast<const double*>(margin), rows, f->K, f->transform, f->tparam,
+                       static_cast<double*>(out));
+  else
+    hipLaunchKernelGGL(transform_rows_kernel<float>, dim3(grid), dim3(threads), 0, s,
+                       static_cast<const float*>(margin), rows, f->K, f->transform, f->tparam,
+                       static_cast<float*>(out));
+  TI_HIP(hipGetLastError());
+  return TI_OK;
+}
+
 int ti_predict_device(ti_forest* f, int32_t slot, const void* X, int32_t xdt, int64_t rows,
                       int32_t cols, int64_t stride, int32_t kind, void* out, int64_t out_len,
                       void* stream) {

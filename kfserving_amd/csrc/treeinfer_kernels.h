@@ -45,6 +45,9 @@
 #ifndef TI_PF
 #define TI_PF 8     // 16-byte words per thread prefetched for the next tree stage
 #endif
+#ifndef TI_NT_X
+#define TI_NT_X 0   // binned staging: non-temporal (streaming) feature loads
+#endif
 
 namespace ti {
 
@@ -527,7 +530,12 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
       const uint32_t r = e / ukc;
       const uint32_t c = e - r * ukc;
       const int f = f0 + (int)c;
+#if TI_NT_X
+      const XT v = f < C ? __builtin_nontemporal_load(X + (row0 + r) * a.row_stride + f)
+                         : nan_value<XT>();
+#else
       const XT v = f < C ? X[(row0 + r) * a.row_stride + f] : nan_value<XT>();
+#endif
       temp[c * R + r] = zero_map(v, a.lgb_zero_map);
     }
     __syncthreads();

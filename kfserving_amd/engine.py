@@ -27,7 +27,8 @@ LIB_PATH = os.environ.get("TREEINFER_LIB", os.path.join(_LIB_DIR, "libtreeinfer.
 
 EXPORTED_SYMBOLS = (
     "ti_forest_create", "ti_forest_destroy", "ti_forest_get_info", "ti_output_shape",
-    "ti_predict", "ti_predict_device", "ti_last_error", "ti_device_count", "ti_abi_version",
+    "ti_predict", "ti_predict_device", "ti_transform_device", "ti_last_error", "ti_device_count",
+    "ti_abi_version",
 )
 
 
@@ -120,6 +121,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.ti_predict.argtypes = [vp, vp, i32, i64, i32, i64, i32, vp, i64]
         lib.ti_predict_device.restype = ctypes.c_int
         lib.ti_predict_device.argtypes = [vp, i32, vp, i32, i64, i32, i64, i32, vp, i64, vp]
+        lib.ti_transform_device.restype = ctypes.c_int
+        lib.ti_transform_device.argtypes = [vp, i32, vp, i64, vp, i64, vp]
         if lib.ti_abi_version() != ABI_VERSION:
             raise TreeInferError(-1, f"ABI mismatch: library {lib.ti_abi_version()}, "
                                      f"binding {ABI_VERSION}")
@@ -250,6 +253,13 @@ class DeviceForest:
         _check(self._lib, self._lib.ti_predict_device(self._handle, slot, x_ptr, x_dtype, n_rows,
                                                       n_cols, row_stride, kind, out_ptr, out_len,
                                                       stream or None))
+
+    def transform_device(self, margin_ptr: int, n_rows: int, out_ptr: int, out_len: int,
+                         slot: int = 0, stream: int = 0) -> None:
+        """Enqueue the output transform over [n_rows, n_groups] device margins
+        (ti_transform_device; the tree-sharded mode's last step)."""
+        _check(self._lib, self._lib.ti_transform_device(self._handle, slot, margin_ptr, n_rows,
+                                                        out_ptr, out_len, stream or None))
 
     def close(self) -> None:
         if getattr(self, "_handle", None) is not None and self._handle.value:

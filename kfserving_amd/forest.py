@@ -182,6 +182,26 @@ class Forest:
             self.cat_nwords = np.ascontiguousarray(self.cat_nwords, dtype=np.int32)
         return self
 
+    def tree_subset(self, t0: int, t1: int, keep_base: bool = True) -> "Forest":
+        """Trees [t0, t1) as a forest of their own (same features, groups,
+        transform and divisor); base margin zeroed unless ``keep_base`` -- one
+        rank's shard in the tree-sharded mode (tree_shard.py)."""
+        import dataclasses
+        if not (0 <= t0 < t1 <= self.n_trees):
+            raise ValueError(f"bad tree range [{t0}, {t1}) of {self.n_trees}")
+        s = slice(int(self.tree_offset[t0]), int(self.tree_offset[t1]))
+        cut = lambda a: None if a is None else np.ascontiguousarray(a[s])   # noqa: E731
+        return dataclasses.replace(
+            self, tree_offset=self.tree_offset[t0:t1 + 1] - self.tree_offset[t0],
+            tree_group=np.ascontiguousarray(self.tree_group[t0:t1]),
+            feature=cut(self.feature), threshold=cut(self.threshold), flags=cut(self.flags),
+            left=cut(self.left), right=cut(self.right), leaf_id=cut(self.leaf_id),
+            leaf_value=cut(self.leaf_value), cover=cut(self.cover),
+            cat_offset=cut(self.cat_offset), cat_nwords=cut(self.cat_nwords),
+            base_margin=(self.base_margin.copy() if keep_base
+                         else np.zeros_like(self.base_margin)),
+            meta=dict(self.meta))
+
     @property
     def has_categorical(self) -> bool:
         return bool(np.any((self.flags & NODE_CATEGORICAL) != 0))

@@ -122,3 +122,29 @@ def sk_predict(trees, value_width, n_features, X, average=True, nthread=0):
       ctypes.c_int64(X.shape[0]), ctypes.c_int32(X.shape[1]), _p(out),
       ctypes.c_int32(1 if average else 0), ctypes.c_int32(nthread))
     return out
+
+
+def tree_shap(f, X, nthread=0):
+    """TreeSHAP contributions of a canonical Forest (oracle/c/shap_port.c),
+    [rows, K * (F + 1)] float64 -- the same layout as TI_OUTPUT_CONTRIB."""
+    if f.cover is None:
+        raise ValueError("forest has no node covers")
+    L = lib()
+    fn = L.port_tree_shap
+    fn.restype = ctypes.c_int
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    out = np.empty((X.shape[0], f.n_groups * (f.n_features + 1)), dtype=np.float64)
+    arrs = [np.ascontiguousarray(a, dtype=dt) for a, dt in (
+        (f.tree_offset, np.int64), (f.tree_group, np.int32), (f.feature, np.int32),
+        (f.threshold, np.float64), (f.flags, np.uint8), (f.left, np.int32),
+        (f.right, np.int32), (f.leaf_value, np.float64), (f.cover, np.float64),
+        (f.base_margin, np.float64))]
+    rc = fn(ctypes.c_int32(f.n_trees), *[_p(a) for a in arrs[:9]],
+            ctypes.c_int32(f.leaf_width), ctypes.c_int32(f.n_groups),
+            ctypes.c_int32(f.n_features), _p(arrs[9]), ctypes.c_double(f.average_divisor),
+            ctypes.c_int32(1 if f.lgb_zero_map else 0), ctypes.c_int32(int(f.depths().max())),
+            _p(X), ctypes.c_int64(X.shape[0]), ctypes.c_int32(X.shape[1]), _p(out),
+            ctypes.c_int32(nthread))
+    if rc:
+        raise MemoryError("port_tree_shap failed")
+    return out

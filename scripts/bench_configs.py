@@ -204,6 +204,82 @@ def c4(args, world, rank):
                              "threads": n_thr, "sample_rows": Xc.shape[0]}}
 
 
+def shap(args, world, rank):
+    """TreeSHAP contributions (TI_OUTPUT_CONTRIB) of the C2 model: 500 trees
+    depth 8, 28 features; work per row = sum over the 128k root-to-leaf paths
+    of O(len^2) path-weight updates (len <= 8 unique features)."""
+    import torch
+    from kfserving_amd.engine import DeviceForest
+    from kfserving_amd.formats import xgboost_format as xf
+    from kfserving_amd.forest import OUT_CONTRIB, TI_F32
+    from oracle import port
+    trees, ti = xf.synthetic_complete_trees(500, 8, 28, seed=0)
+    f = xf.forest_from_raw_trees(trees, ti, 28, 0, 0.5, "binary:logistic")
+    dev = DeviceForest(f, [torch.cuda.current_device()])
+    lo, hi = shard(args.rows_shap, world, rank)
+    rows = hi - lo
+    X = device_normal(rows, 28, seed=5 + rank)
+    W = 29
+    out = torch.empty(rows * W, dtype=torch.float32, device="cuda")
+    step_s, kms = time_device(dev, X, out, rows, 28, OUT_CONTRIB, TI_F32, args.steps, 1)
+    if rank != 0:
+        return None
+    n = min(rows, 2000)
+    Xs = X[:n].cpu().numpy()
+    t0 = time.perf_counter()
+    want = port.tree_shap(f, Xs.astype(np.float64))
+    cpu = n / (time.perf_counter() - t0)
+    got = out[:n * W].cpu().numpy().reshape(n, W).astype(np.float64)
+    scale = np.maximum(np.abs(want).max(axis=1, keepdims=True), 1.0)
+    return {"config": "TreeSHAP contributions of the C2 model (500 x depth 8, 28 feat)",
+            "rows": args.rows_shap, "n_gpus": world, "rows_per_gpu": rows, "scaling": "strong",
+            "rows_per_s": args.rows_shap / step_s, "step_ms": step_s * 1e3, "kernel_ms": kms,
+            "max_scaled_err_vs_port": float((np.abs(got - want) / scale).max()),
+            "parity_rows": n,
+            "cpu_baseline": {"rows_per_s": cpu, "kind": "port (oracle/c/shap_port.c)",
+                             "threads": port.num_threads(), "sample_rows": n}}
+
+
+def ts(args, world, rank):
+    """Tree-sharded C2 (kfserving_amd/tree_shard.py): every rank predicts the
+    same 1M rows over its 500/world trees, partial margins summed by one
+    RCCL reduce to rank 0, transform there.  Strong scaling in trees."""
+    import torch
+    import torch.distributed as dist
+    from kfserving_amd.formats import xgboost_format as xf
+    from kfserving_amd.forest import OUT_PREDICT
+    from kfserving_amd.tree_shard import TreeShardedForest
+    trees, ti = xf.synthetic_complete_trees(500, 8, 28, seed=0)
+    f = xf.forest_from_raw_trees(trees, ti, 28, 0, 0.5, "binary:logistic")
+    sh = TreeShardedForest(f, device=torch.cuda.current_device())
+    X = device_normal(args.rows_ts, 28, seed=0)
+    for _ in range(2):
+        sh.predict(X, OUT_PREDICT)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = sh.predict(X, OUT_PREDICT)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    wall = max_over_ranks(time.perf_counter() - t0) / args.steps
+    if rank != 0:
+        return None
+    from kfserving_amd.engine import DeviceForest
+    ref = torch.empty_like(out)
+    DeviceForest(f, [torch.cuda.current_device()]).predict_device(
+        X.data_ptr(), 0, args.rows_ts, 28, 28, OUT_PREDICT, ref.data_ptr(), ref.numel(),
+        stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    err = float(((out - ref).abs() / ref.abs().clamp_min(1e-30)).max())
+    return {"config": "C2 tree-sharded (trees split over ranks, RCCL reduce of margins)",
+            "rows": args.rows_ts, "n_gpus": world, "trees_per_rank": [b - a for a, b in sh.ranges],
+            "scaling": "strong", "rows_per_s": args.rows_ts / wall, "step_ms": wall * 1e3,
+            "max_rel_err_vs_one_device": err}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--configs", default="c3,c4")
@@ -212,6 +288,8 @@ def main():
     p.add_argument("--rows4", type=int, default=10_000_000)
     p.add_argument("--fit-rows", type=int, default=200_000)
     p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--rows-shap", type=int, default=100_000)
+    p.add_argument("--rows-ts", type=int, default=1_000_000)
     args = p.parse_args()
     import torch  # noqa: F401  (one HIP runtime: torch's, loaded first)
     import torch.distributed as dist
@@ -220,7 +298,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
     for c in args.configs.split(","):
-        res = {"c3": c3, "c4": c4}[c.strip()](args, world, rank)
+        res = {"c3": c3, "c4": c4, "shap": shap, "ts": ts}[c.strip()](args, world, rank)
         if res is not None:
             print(json.dumps(res), flush=True)
     if world > 1:

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 run() {  # name timeout args...
   local name=$1 to=$2; shift 2
   echo "== $name" | tee -a "$OUT/steps.log"
-  (cd /tmp && timeout -k 10 "$to" rocprofv3 "$@" -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --latency-qps 0) > "$OUT/$name.log" 2>&1
+  (cd /tmp && timeout -k 10 "$to" rocprofv3 "$@" -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --latency-qps 0 --nan-variant 0) > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "rc=$rc $name" | tee -a "$OUT/steps.log"
   tail -2 "$OUT/$name.log"

@@ -73,7 +73,17 @@ def predict(f, X, kind=1):
     m = acc if f.base_first else (f.base_margin.astype(acc_t) + acc)
     if f.average_divisor != 1.0:
         m = m / acc_t(f.average_divisor)
-    if kind == OUT_MARGIN or f.transform == T_IDENTITY:
+    if kind == OUT_MARGIN:
+        return m if K > 1 else m[:, 0]
+    return transform(f, m)
+
+
+def transform(f, m):
+    """The output transform over [rows, K] margins of the accumulation type."""
+    acc_t = np.float32 if f.accum_dtype == TI_F32 else np.float64
+    K = f.n_groups
+    m = np.asarray(m, dtype=acc_t).reshape(-1, K)
+    if f.transform == T_IDENTITY:
         return m if K > 1 else m[:, 0]
     if f.transform == T_ARGMAX:
         return np.argmax(m, axis=1).astype(acc_t)

@@ -75,3 +75,18 @@ def test_efficiency(make):
     c = shap_ref.contributions(f, X).reshape(X.shape[0], f.n_groups, f.n_features + 1)
     margin = canon_eval.predict(f, X, OUT_MARGIN).reshape(X.shape[0], f.n_groups)
     np.testing.assert_allclose(c.sum(axis=2), margin, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("make", [
+    lambda: _xgb(20, 6, 8, seed=4),
+    lambda: _xgb(6, 4, 5, seed=8, K=3),
+    lambda: _lgb(10, 63, 12, seed=6, K=3),
+    lambda: _sk_forest(),
+], ids=["xgb", "xgb-multiclass", "lgb-multiclass", "sklearn"])
+def test_c_port_matches_restatement(make):
+    """oracle/c/shap_port.c (the CPU baseline) == the numpy restatement."""
+    from oracle import port
+    f = make()
+    X = _rows(f.n_features, 50, seed=9)
+    np.testing.assert_allclose(port.tree_shap(f, X, nthread=2), shap_ref.contributions(f, X),
+                               rtol=1e-12, atol=1e-12)
