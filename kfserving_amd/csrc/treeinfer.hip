@@ -291,7 +291,15 @@ struct ti_forest {
     int32_t b16 = 1;
     int32_t rows = 256;
     int32_t words = 0;
+    std::vector<unsigned char> sx;   // staged slot image (layout 5): [T][sx_slots] x 8 B
   } bx[2];
+  // staged binned explicit (layout 5): slots per tree record (even, so records
+  // stay 16-byte aligned), the slot of every descriptor node, per-slot leaf
+  // values (ACC) and leaf ids
+  int64_t sx_slots = 0;
+  std::vector<int32_t> h_sx_slot;
+  std::vector<unsigned char> h_sx_vals;
+  std::vector<int32_t> h_sx_ids;
   int32_t bx_ilp = 4;               // trees per lane in lockstep (4 or 8)
   std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
   // TreeSHAP (TI_OUTPUT_CONTRIB); has_shap = 0 when the forest has no covers
@@ -819,9 +827,58 @@ bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
   return true;
 }
 
-// Rank-coded copy of the explicit nodes (pack_explicit must have run).
-// Returns false when a feature has more than 65,533 distinct thresholds or the
-// bin image does not fit 64 KB even at 64-row tiles.
+// Slots of the staged explicit layout (see kSxLeaf): breadth-first, the root in
+// slot 0 and the children of each internal node in the next two free slots.
+// Leaves back per-slot value / id tables.  Leaves f->sx_slots = 0 when a tree
+// has more than kSxMaxSlots nodes (its record would not leave room in LDS).
+constexpr int64_t kSxMaxSlots = 1024;
+void plan_slots(const ti_forest_desc* d, ti_forest* f) {
+  f->sx_slots = 0;
+  int64_t ns = 0;
+  for (int t = 0; t < d->n_trees; ++t) ns = std::max(ns, d->tree_offset[t + 1] - d->tree_offset[t]);
+  ns = (ns + 1) & ~int64_t(1);
+  if (ns > kSxMaxSlots) return;
+  const int LW = d->leaf_width;
+  const size_t as = f->accum == TI_F64 ? 8 : 4;
+  f->h_sx_slot.assign(d->n_nodes, 0);
+  f->h_sx_vals.assign(static_cast<size_t>(d->n_trees) * ns * LW * as, 0);
+  f->h_sx_ids.assign(static_cast<size_t>(d->n_trees) * ns, 0);
+  std::vector<int32_t> q;
+  for (int t = 0; t < d->n_trees; ++t) {
+    const int64_t b = d->tree_offset[t];
+    q.assign(1, 0);
+    int32_t next = 1;
+    for (size_t qi = 0; qi < q.size(); ++qi) {
+      const int64_t g = b + q[qi];
+      if (d->feature[g] < 0) continue;
+      f->h_sx_slot[b + d->left[g]] = next;
+      f->h_sx_slot[b + d->right[g]] = next + 1;
+      next += 2;
+      q.push_back(d->left[g]);
+      q.push_back(d->right[g]);
+    }
+    for (int64_t g = b; g < d->tree_offset[t + 1]; ++g) {
+      if (d->feature[g] >= 0) continue;
+      const size_t s = static_cast<size_t>(t) * ns + f->h_sx_slot[g];
+      f->h_sx_ids[s] = d->leaf_id[g];
+      for (int k = 0; k < LW; ++k) {
+        const double v = d->leaf_value[g * LW + k];
+        if (as == 8) {
+          std::memcpy(&f->h_sx_vals[(s * LW + k) * 8], &v, 8);
+        } else {
+          const float v32 = static_cast<float>(v);
+          std::memcpy(&f->h_sx_vals[(s * LW + k) * 4], &v32, 4);
+        }
+      }
+    }
+  }
+  f->sx_slots = ns;
+}
+
+// Rank-coded copy of the explicit nodes (pack_explicit must have run), and of
+// the staged slots when plan_slots accepted the trees.  Returns false when a
+// feature has more than 65,533 distinct thresholds or the bin image does not
+// fit 64 KB even at 64-row tiles.
 template <typename XT>
 bool pack_bexplicit(const ti_forest_desc* d, ti_forest* f, ti_forest::BinExplicit* bx) {
   const RankTables<XT> rt = collect_ranks<XT>(d, f->zero_rule != 0);
@@ -847,6 +904,33 @@ bool pack_bexplicit(const ti_forest_desc* d, ti_forest* f, ti_forest::BinExplici
     if (d->flags[g] & TI_NODE_NAN_LEFT) e.meta |= ti::kMetaNanLeft;
     if (zflip) e.meta |= ti::kMetaZeroFlip;
     bx->nodes[i] = e;
+  }
+  bx->sx.clear();
+  if (f->sx_slots > 0) {   // the same nodes as staged slots (layout 5)
+    const int64_t ns = f->sx_slots;
+    bx->sx.assign(static_cast<size_t>(d->n_trees) * ns * 8, 0);
+    for (int t = 0; t < d->n_trees; ++t) {
+      const int64_t b = d->tree_offset[t];
+      const int64_t n = d->tree_offset[t + 1] - b;
+      for (int64_t s = 0; s < ns; ++s) {   // every slot a self-loop leaf until filled
+        const uint32_t rec[2] = {ti::kSxLeaf, ti::kSxNanLeft | static_cast<uint32_t>(s)};
+        std::memcpy(&bx->sx[(t * ns + s) * 8], rec, 8);
+      }
+      for (int64_t v = 0; v < n; ++v) {
+        const int64_t g = b + v;
+        const int fe = d->feature[g];
+        if (fe < 0) continue;
+        const bool zflip = (d->flags[g] & TI_NODE_ZERO_FLIP) != 0;
+        const uint32_t off = static_cast<uint32_t>((fe / P) * R * 4 + (fe % P) * (4 / P));
+        if (off > 0xFFFFu) return false;
+        uint32_t rec[2];
+        rec[0] = (rt.rank(fe, d->threshold[g]) << 16) | off;
+        rec[1] = ((zflip ? rt.zbin[fe] : 0u) << 16) |
+                 ((d->flags[g] & TI_NODE_NAN_LEFT) ? ti::kSxNanLeft : 0u) |
+                 static_cast<uint32_t>(f->h_sx_slot[b + d->left[g]]);
+        std::memcpy(&bx->sx[(t * ns + f->h_sx_slot[g]) * 8], rec, 8);
+      }
+    }
   }
   return true;
 }
@@ -972,6 +1056,15 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
     if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
     d.leaves = lv;
     if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
+  } else if (f->layout == 5) {
+    for (int i = 0; i < 2; ++i) {
+      if ((rc = upload(&d.bh_img[i], f->bx[i].sx, &d.bytes))) return rc;
+      if ((rc = upload(&d.bx_tbl[i], f->bx[i].tbl, &d.bytes))) return rc;
+    }
+    unsigned char* lv = nullptr;
+    if ((rc = upload(&lv, f->h_sx_vals, &d.bytes))) return rc;
+    d.leaves = lv;
+    if ((rc = upload(&d.exp_leaf_ids, f->h_sx_ids, &d.bytes))) return rc;
   } else if (f->layout == 3) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.bh_img[i], f->bh[i].img, &d.bytes))) return rc;
@@ -1030,6 +1123,13 @@ KernelFn select_bexplicit(int xdt, int accum, int K, bool b16, bool z, int ilp) 
   return ti::kernels_df(4, K, true, z, b16, ilp);
 }
 
+KernelFn select_sexplicit(int xdt, int accum, int K, bool b16, bool z, int ilp) {
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(5, K, true, z, b16, ilp);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(5, K, true, z, b16, ilp);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(5, K, true, z, b16, ilp);
+  return ti::kernels_df(5, K, true, z, b16, ilp);
+}
+
 std::mutex g_attr_mu;
 std::set<std::pair<int, const void*>> g_attr_done;
 
@@ -1079,7 +1179,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     R = ci.feat_lds ? ci.rows : 0;
   } else if (f->layout == 3) {
     R = f->bh[xdt == TI_F64 ? 1 : 0].rows;
-  } else if (f->layout == 4) {
+  } else if (f->layout == 4 || f->layout == 5) {
     R = f->bx[xdt == TI_F64 ? 1 : 0].rows;
   } else {
     R = 256;
@@ -1090,7 +1190,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   if (!feat_lds) R = 256;
   size_t feat_bytes = feat_lds ? align16(static_cast<size_t>(f->F) * R * xs) : 0;
   if (f->layout == 3) feat_bytes = static_cast<size_t>(f->bh[xdt == TI_F64 ? 1 : 0].words) * R * 4;
-  if (f->layout == 4) feat_bytes = static_cast<size_t>(f->bx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
+  if (f->layout == 4 || f->layout == 5)
+    feat_bytes = static_cast<size_t>(f->bx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
 
   KArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1204,6 +1305,37 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.bin_words = bx.words;
     lds = feat_bytes + 16;
     KernelFn fn = select_bexplicit(xdt, f->accum, f->K, bx.b16 != 0, f->zero_rule != 0, f->bx_ilp);
+    int rc = ensure_lds_attr(d.device, fn);
+    if (rc) return rc;
+    const int64_t grid = (rows + R - 1) / R;
+    if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    TI_HIP(hipGetLastError());
+    return TI_OK;
+  } else if (f->layout == 5) {
+    // stage: S trees, as many as the prefetch registers carry (8 x 16 B per
+    // thread), at least one
+    const int ii = xdt == TI_F64 ? 1 : 0;
+    const ti_forest::BinExplicit& bx = f->bx[ii];
+    const int64_t stride_b = f->sx_slots * 8;
+    if (R > 256 || stride_b > static_cast<int64_t>(8) * 16 * R)
+      return fail(TI_ERR_UNSUPPORTED, "staged explicit layout needs <= 256-row tiles");
+    int64_t S = static_cast<int64_t>(8) * 16 * R / stride_b;
+    static const int force_s = env_int("TI_SX_STAGE", 0);
+    if (force_s > 0) S = std::min<int64_t>(force_s, S);
+    S = std::min<int64_t>(S, f->T);
+    a.trees = d.bh_img[ii];
+    a.tree_stride = stride_b;
+    a.stage_trees = static_cast<int32_t>(S);
+    a.leaves = d.leaves;
+    a.exp_leaf_ids = d.exp_leaf_ids;
+    a.bin_tbl = d.bx_tbl[ii];
+    a.bin_L = bx.L;
+    a.bin_words = bx.words;
+    a.stage_off = static_cast<int32_t>(align16(feat_bytes + 4));
+    lds = static_cast<size_t>(a.stage_off) + static_cast<size_t>(S * stride_b);
+    if (lds > kLdsPerCu) return fail(TI_ERR_UNSUPPORTED, "staged explicit layout exceeds LDS");
+    KernelFn fn = select_sexplicit(xdt, f->accum, f->K, bx.b16 != 0, f->zero_rule != 0, f->bx_ilp);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -1646,7 +1778,10 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   bool use_compact = false;
   if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
   if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
-  if (want == "explicit" || want == "bexplicit") { use_heap = false; use_compact = false; }
+  if (want == "explicit" || want == "bexplicit" || want == "sexplicit") {
+    use_heap = false;
+    use_compact = false;
+  }
   // categorical splits are evaluated by the explicit kernel only
   if (f->has_cat) { use_heap = false; use_compact = false; }
   if (use_compact) {
@@ -1712,6 +1847,9 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
     // rank-binned explicit nodes unless a categorical split needs raw values
     // (TI_FORCE_LAYOUT=explicit keeps the float-compare kernel)
     if (!f->has_cat && want != "explicit" && env_int("TI_NO_BEXPLICIT", 0) == 0) {
+      // the LDS-staged walk (layout 5) is opt-in: at C3's F = 100 the stage costs
+      // the third workgroup per CU and the walk runs 0.65x layout 4
+      if (want == "sexplicit") plan_slots(desc, f.get());
       if (pack_bexplicit<float>(desc, f.get(), &f->bx[0]) &&
           pack_bexplicit<double>(desc, f.get(), &f->bx[1])) {
         f->layout = 4;
@@ -1745,6 +1883,12 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         f->bx_ilp = mean_depth < 12.0 ? 8 : 4;
         const int force_ilp = env_int("TI_BEXP_ILP", 0);
         if (force_ilp > 0) f->bx_ilp = force_ilp >= 8 ? 8 : 4;
+        // trees small enough to stage in LDS walk from the stage (layout 5)
+        if (f->sx_slots > 0 && !f->bx[0].sx.empty() && !f->bx[1].sx.empty()) {
+          f->layout = 5;
+          const int force_sx = env_int("TI_SX_ILP", 0);
+          f->bx_ilp = force_sx > 0 ? (force_sx >= 8 ? 8 : 4) : 8;
+        }
       } else {
         for (auto& bx : f->bx) bx = ti_forest::BinExplicit();
       }
@@ -1771,7 +1915,12 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
     ci.img.clear();
     ci.img.shrink_to_fit();
   }
+  f->h_sx_slot.clear(); f->h_sx_slot.shrink_to_fit();
+  f->h_sx_vals.clear(); f->h_sx_vals.shrink_to_fit();
+  f->h_sx_ids.clear(); f->h_sx_ids.shrink_to_fit();
   for (auto& bx : f->bx) {
+    bx.sx.clear();
+    bx.sx.shrink_to_fit();
     bx.nodes.clear();
     bx.nodes.shrink_to_fit();
     bx.tbl.clear();

@@ -9,11 +9,26 @@ namespace ti {
 
 using KernelFn = void (*)(KArgs);
 
-// layout: 0 heap, 1 explicit, 2 compact, 3 binned heap, 4 binned explicit.  fl: feature image in
+// layout: 0 heap, 1 explicit, 2 compact, 3 binned heap, 4 binned explicit,
+// 5 staged binned explicit.  fl: feature image in
 // LDS; z: LightGBM zero rule; b16 / pf: binned heap bin width and prefetch
 // depth.
 template <typename XT, typename ACC, int KMAX>
 KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
+  if (layout == 5) {   // pf carries the tree ILP (4 or 8)
+    if constexpr (sizeof(ACC) == 8) {
+      if (z) {
+        if (pf >= 8) return b16 ? sexplicit_predict_kernel<XT, ACC, KMAX, true, true, 8>
+                                : sexplicit_predict_kernel<XT, ACC, KMAX, false, true, 8>;
+        return b16 ? sexplicit_predict_kernel<XT, ACC, KMAX, true, true, 4>
+                   : sexplicit_predict_kernel<XT, ACC, KMAX, false, true, 4>;
+      }
+    }
+    if (pf >= 8) return b16 ? sexplicit_predict_kernel<XT, ACC, KMAX, true, false, 8>
+                            : sexplicit_predict_kernel<XT, ACC, KMAX, false, false, 8>;
+    return b16 ? sexplicit_predict_kernel<XT, ACC, KMAX, true, false, 4>
+               : sexplicit_predict_kernel<XT, ACC, KMAX, false, false, 4>;
+  }
   if (layout == 4) {   // pf carries the tree ILP (4 or 8)
     if constexpr (sizeof(ACC) == 8) {
       if (z) {

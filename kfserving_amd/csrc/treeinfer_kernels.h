@@ -1080,4 +1080,125 @@ __global__ void __launch_bounds__(512) bexplicit_predict_kernel(const KArgs a) {
   finish_row<ACC, KMAX>(acc, a, row);
 }
 
+// ---- staged binned explicit (layout 5) -------------------------------------
+// Irregular trees small enough to stage in LDS (LightGBM leaf-wise, C3): the
+// binned explicit walk of bexplicit_predict_kernel with the nodes read from an
+// LDS stage instead of global memory, so a step is two LDS reads and ~6 VALU
+// instead of a 16-byte gather through the vector L1 (the gathers bounded the
+// global-memory walk: 54 % of wave cycles waiting, rocprofv3 C3 profile).
+//
+// A tree record is tree_stride / 8 slots of 8 bytes.  Slot 0 is the root and
+// the two children of an internal node sit in consecutive slots (left, then
+// right), so the next slot is left + (went right).  Internal slot:
+//   x = rank << 16 | bin byte offset (the lane-free part, as in bheap);
+//   y = zbin << 16 | NaN-left << 15 | left child slot (15 bits).
+// Leaf slot: x = kSxLeaf (rank 0xFFFF: no bin goes right of it), y = NaN-left
+// | its own slot, so a lane that reached its leaf stays on it while the rest of
+// the wave finishes the tree group.  Leaf values / ids are per-slot global
+// tables ([T][slots]), read once per tree.
+constexpr uint32_t kSxLeaf = 0xFFFF0000u;
+constexpr uint32_t kSxNanLeft = 0x8000u;
+constexpr uint32_t kSxSlotMask = 0x7FFFu;
+
+struct SxRec {
+  uint32_t x, y;
+};
+__device__ __forceinline__ SxRec lds_u2(uint32_t byte_addr) {
+  const uint64_t v = *reinterpret_cast<const __attribute__((address_space(3))) uint64_t*>(
+      static_cast<uintptr_t>(byte_addr));
+  return SxRec{(uint32_t)v, (uint32_t)(v >> 32)};
+}
+
+template <typename ACC, int KMAX, bool B16, bool ZERO, bool CHECK_NAN, int ILP>
+__device__ __forceinline__ void sx_stage(const KArgs& a, int cnt, int t0, ACC (&acc)[KMAX],
+                                         uint32_t lane_off, int64_t row, bool live) {
+  using BT = BinTraits<B16>;
+  const int T = a.n_trees;
+  const uint32_t stride = (uint32_t)a.tree_stride;
+  const int64_t nslot = a.tree_stride >> 3;
+  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
+  const ACC* vals = static_cast<const ACC*>(a.leaves);
+  for (int j = 0; j < cnt; j += ILP) {
+    uint32_t base[ILP], slot[ILP];
+    SxRec rec[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = (j + q) < cnt ? (j + q) : (cnt - 1);
+      base[q] = (uint32_t)a.stage_off + (uint32_t)tq * stride;
+      slot[q] = 0u;
+      rec[q] = lds_u2(base[q]);
+    }
+    for (;;) {
+      uint32_t b[ILP];
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) b[q] = lds_bin<B16>((rec[q].x & 0xFFFFu) | lane_off);
+      bool active = false;
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        bool right = (rec[q].x >> 16) < b[q];
+        if (ZERO) right = right != (b[q] == (rec[q].y >> 16));
+        if (CHECK_NAN && b[q] == BT::kNan) right = (rec[q].y & kSxNanLeft) == 0u;
+        slot[q] = (rec[q].y & kSxSlotMask) + (right ? 1u : 0u);
+        rec[q] = lds_u2(base[q] + slot[q] * 8u);
+        active |= rec[q].x < kSxLeaf;
+      }
+      if (__ballot(active) == 0) break;
+    }
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      if (j + q < cnt) {
+        const int t = t0 + j + q;
+        if (want_leaf) {
+          if (live) static_cast<int32_t*>(a.out)[row * T + t] = a.exp_leaf_ids[(int64_t)t * nslot + slot[q]];
+        } else {
+          add_leaf<ACC, KMAX>(acc, vals + (int64_t)t * nslot * a.leaf_width, (int)slot[q],
+                              a.leaf_width, a.tree_group[t]);
+        }
+      }
+    }
+  }
+}
+
+template <typename XT, typename ACC, int KMAX, bool B16, bool ZERO, int ILP>
+__global__ void __launch_bounds__(256) sexplicit_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int PF = 8;
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  unsigned char* stage = smem + a.stage_off;
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  const int T = a.n_trees;
+  const int S = a.stage_trees;
+  const int64_t stride = a.tree_stride;
+  u32x4 pf[PF];
+  prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees),
+                 (int)(((int64_t)(T < S ? T : S) * stride) >> 4), tid, R);
+  const bool tile_nan = stage_bins_rows<XT, B16>(flag, a, row0, R, tid);
+  ACC acc[KMAX];
+  init_acc(acc, a);
+  const int last0 = ((T - 1) / S) * S;
+  for (int t0 = 0; t0 < T; t0 += S) {
+    const int cnt = (T - t0) < S ? (T - t0) : S;
+    __syncthreads();
+    commit_n<PF>(pf, reinterpret_cast<u32x4*>(stage), (int)(((int64_t)cnt * stride) >> 4), tid, R);
+    __syncthreads();
+    {
+      const int tn = t0 + S <= last0 ? t0 + S : last0;
+      const int cn = (T - tn) < S ? (T - tn) : S;
+      prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees + (int64_t)tn * stride),
+                     (int)(((int64_t)cn * stride) >> 4), tid, R);
+    }
+    if (tile_nan)
+      sx_stage<ACC, KMAX, B16, ZERO, true, ILP>(a, cnt, t0, acc, lane_off, row, live);
+    else
+      sx_stage<ACC, KMAX, B16, ZERO, false, ILP>(a, cnt, t0, acc, lane_off, row, live);
+  }
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
 }  // namespace ti

@@ -340,10 +340,11 @@ def _dev_with_layout(forest, layout):
             os.environ["TI_FORCE_LAYOUT"] = old
 
 
-LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2, "bheap": 3, "bexplicit": 4}
+LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2, "bheap": 3, "bexplicit": 4, "sexplicit": 5}
 
 
-@pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit"])
+@pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
+                                    "sexplicit"])
 def test_xgb_golden_every_layout(golden, layout):
     g = np.load(os.path.join(golden, "xgb_synth.npz"))
     trees, ti = xf.synthetic_complete_trees(40, 8, 28, seed=1)
@@ -359,7 +360,7 @@ def test_xgb_golden_every_layout(golden, layout):
     np.testing.assert_allclose(dev3.predict(g["X"], OUT_PREDICT), g["prob3"], rtol=RTOL)
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit"])
+@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
     g = np.load(os.path.join(golden, "lgb_synth.npz"))
@@ -376,7 +377,8 @@ def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
     assert np.array_equal(dev.predict(X, OUT_LEAF), lgb_ref.leaf_index(lm, Xd))
 
 
-@pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit"])
+@pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
+                                    "sexplicit"])
 def test_lgb_iris_fixture_every_layout(golden, layout):
     from sklearn.datasets import load_iris
     path = os.path.join(golden, "lgb_iris_v3.txt")
@@ -386,7 +388,7 @@ def test_lgb_iris_fixture_every_layout(golden, layout):
     assert np.array_equal(dev.predict(X, OUT_MARGIN), lgb_ref.predict(m, X, raw_score=True))
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit"])
+@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit"])
 def test_sklearn_classifier_every_layout(golden, layout):
     fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
     gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
@@ -418,17 +420,19 @@ def test_compact_ragged_and_specials(rows):
                           port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
 
 
+@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit"])
 @pytest.mark.parametrize("rows", [1, 255, 257, 3000])
-def test_bexplicit_zero_missing_and_specials(rows):
-    """Binned explicit kernel on leaf-wise trees with every missing type: the
-    zero rule runs on a dedicated bin of exact 0 (after the |x| <= 1e-35 map)."""
+def test_bexplicit_zero_missing_and_specials(rows, layout):
+    """Binned explicit kernels (nodes in global memory / staged in LDS) on
+    leaf-wise trees with every missing type: the zero rule runs on a dedicated
+    bin of exact 0 (after the |x| <= 1e-35 map)."""
     trees = lf.synthetic_leafwise_trees(41, 255, 40, seed=7)
     with tempfile.TemporaryDirectory() as d:
         p = os.path.join(d, "model.txt")
         lf.write_lightgbm_text(p, trees, 40, "binary sigmoid:1")
         f = load_lightgbm_model(p)
-    dev = DeviceForest(f, [0])
-    assert dev.info()["layout"] == 4
+    dev = _dev_with_layout(f, layout)
+    assert dev.info()["layout"] == LAYOUT_ID[layout]
     rng = np.random.default_rng(rows + 1)
     X = rng.standard_normal((rows, 40))
     sp = np.array([np.nan, 0.0, -0.0, 1e-40, -1e-36, 1e-35, 2e-35, np.inf, -np.inf])
