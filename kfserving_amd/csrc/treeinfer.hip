@@ -26,6 +26,7 @@
 #include <set>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "treeinfer.h"
@@ -135,6 +136,120 @@ __global__ void __launch_bounds__(64) contrib_kernel(
   ACC* o = out + row * W;
   for (int g = 0; g < K; ++g) {
     for (int f = 0; f < F; ++f) o[g * (F + 1) + f] = (ACC)(ph[g * (F + 1) + f] / divisor);
+    o[g * (F + 1) + F] = (ACC)bias[g];
+  }
+}
+
+// 1/k for k = 0..64 (entry 0 unused), exactly rounded at compile time.
+template <int... I>
+struct ShapInvTable {
+  double v[sizeof...(I)];
+};
+template <int... I>
+constexpr ShapInvTable<I...> make_inv(std::integer_sequence<int, I...>) {
+  return {{(I == 0 ? 0.0 : 1.0 / I)...}};
+}
+__constant__ ShapInvTable kShapInv = make_inv(std::make_integer_sequence<int, 65>{});
+
+// The contrib kernel with the path arithmetic in registers.  Everything about
+// a path (its length, elements, zero fractions, leaf) is the same for all 64
+// lanes, so it comes through scalar loads; a lane only owns its row's one
+// fractions (a bitmask: they are 0 or 1) and its path weights w[0..n], which
+// stay in VGPRs because every loop that indexes them is unrolled over MAXN.
+// The divisions of contrib_kernel become products with compile-time ratios
+// or the 1/k table.  The row's contributions accumulate in LDS [W][64]
+// (W = K * (F + 1) <= kShapLdsW), so no global read-modify-write.
+constexpr int kShapLdsW = 128;
+template <typename XT, typename ACC, int MAXN>
+__global__ void __launch_bounds__(64) contrib_reg_kernel(
+    const XT* __restrict__ X, int64_t rows, int64_t stride, int32_t cols, int32_t zero_map_on,
+    const ShapPath* __restrict__ paths, int64_t n_paths, const ShapElem* __restrict__ elems,
+    const double* __restrict__ leafv, int32_t LW, int32_t K, int32_t F, int32_t maxl,
+    const double* __restrict__ bias, double divisor, double* __restrict__ acc,
+    ACC* __restrict__ out) {
+  (void)maxl;
+  (void)acc;
+  extern __shared__ double shap_lds[];
+  const int lane = threadIdx.x;
+  const int64_t row = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = row < rows;
+  const XT* xr = X + (live ? row : rows - 1) * stride;
+  const int W = K * (F + 1);
+  double* phi = shap_lds + lane;                  // phi[j * 64]
+  for (int j = 0; j < W; ++j) phi[j * 64] = 0.0;
+  for (int64_t p = 0; p < n_paths; ++p) {
+    const ShapPath P = paths[p];
+    const int n = P.n;
+    const ShapElem* pe = elems + P.first;
+    uint32_t om = 0u;                             // one fractions, bit i = element i
+    for (int i = 0; i < n; ++i) {
+      const ShapElem e = pe[i];
+      double x = e.feature < cols ? (double)xr[e.feature] : __builtin_nan("");
+      if (zero_map_on && __builtin_fabs(x) <= (double)1e-35f) x = 0.0;
+      bool follow;
+      if (x != x) follow = (e.flags & kShapNanOk) != 0;
+      else if (x == 0.0) follow = (e.flags & kShapZeroOk) != 0;
+      else follow = !(e.flags & kShapEmpty) && e.lo < x && x <= e.hi;
+      om |= (follow ? 1u : 0u) << i;
+    }
+    // ExtendPath from scratch
+    double w[MAXN + 1];
+    w[0] = 1.0;
+#pragma unroll
+    for (int d = 1; d <= MAXN; ++d) {
+      if (d <= n) {
+        const double of = ((om >> (d - 1)) & 1u) ? 1.0 : 0.0;
+        const double zf = pe[d - 1].zf;
+        w[d] = 0.0;
+#pragma unroll
+        for (int i = d - 1; i >= 0; --i) {
+          w[i + 1] += of * w[i] * ((double)(i + 1) / (double)(d + 1));
+          w[i] = zf * w[i] * ((double)(d - i) / (double)(d + 1));
+        }
+      }
+    }
+    const double rn1 = (double)(n + 1);
+    const double in1 = kShapInv.v[n + 1];
+    double wn = 0.0;                              // w[n]
+#pragma unroll
+    for (int i = 0; i <= MAXN; ++i)
+      if (i == n) wn = w[i];
+    const double* lv = leafv + P.leaf * LW;
+    // UnwoundPathSum per element, times (one - zero) times the leaf value
+    for (int e_i = 0; e_i < n; ++e_i) {
+      const ShapElem e = pe[e_i];
+      const bool one = ((om >> e_i) & 1u) != 0u;
+      const double zf = e.zf;
+      double total = 0.0;
+      if (one) {
+        double next = wn;
+#pragma unroll
+        for (int i = MAXN - 1; i >= 0; --i) {
+          if (i < n) {
+            const double tmp = next * (rn1 * (1.0 / (double)(i + 1)));
+            total += tmp;
+            next = w[i] - tmp * zf * ((double)(n - i) * in1);
+          }
+        }
+      } else {
+        const double izf = 1.0 / zf;
+#pragma unroll
+        for (int i = MAXN - 1; i >= 0; --i) {
+          if (i < n) total += w[i] * izf * (rn1 * kShapInv.v[n - i]);
+        }
+      }
+      const double scale = total * ((one ? 1.0 : 0.0) - zf);
+      if (LW == 1) {
+        phi[(P.group * (F + 1) + e.feature) * 64] += scale * lv[0];
+      } else {
+        for (int k = 0; k < LW; ++k) phi[(k * (F + 1) + e.feature) * 64] += scale * lv[k];
+      }
+    }
+  }
+  if (!live) return;
+  ACC* o = out + row * W;
+  for (int g = 0; g < K; ++g) {
+    for (int f = 0; f < F; ++f) o[g * (F + 1) + f] = (ACC)(phi[(g * (F + 1) + f) * 64] / divisor);
     o[g * (F + 1) + F] = (ACC)bias[g];
   }
 }
@@ -1561,6 +1676,41 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
     return fail(TI_ERR_UNSUPPORTED,
                 "contributions need node covers (ti_forest_desc.cover) and no categorical splits");
   const int64_t W = static_cast<int64_t>(f->K) * (f->F + 1);
+  const int64_t n_paths = static_cast<int64_t>(d.shap_paths ? 1 : 0) * f->shap_npaths;
+  static const int force_generic = env_int("TI_SHAP_GENERIC", 0);
+  if (W <= kShapLdsW && f->shap_maxl <= 32 && !force_generic) {
+    // registers + LDS accumulators: no scratch accumulator, no memset
+    const int maxn = f->shap_maxl <= 8 ? 8 : f->shap_maxl <= 16 ? 16 : 32;
+    const size_t lds_w = static_cast<size_t>(W) * 64 * 8;
+    const unsigned grid_r = static_cast<unsigned>((rows + 63) / 64);
+    if (rows == 0) return TI_OK;
+#define TI_CONTRIB_REG(XT_, ACC_, N_)                                                          \
+  do {                                                                                         \
+    int rc_ = ensure_lds_attr(d.device, reinterpret_cast<KernelFn>(contrib_reg_kernel<XT_, ACC_, N_>)); \
+    if (rc_) return rc_;                                                                       \
+    hipLaunchKernelGGL((contrib_reg_kernel<XT_, ACC_, N_>), dim3(grid_r), dim3(64), lds_w, stream, \
+                       static_cast<const XT_*>(X), rows, stride, cols, f->lgb_zero_map,        \
+                       d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,    \
+                       f->shap_maxl, d.shap_bias, f->divisor, nullptr, static_cast<ACC_*>(out)); \
+  } while (0)
+#define TI_CONTRIB_REG_N(XT_, ACC_)                          \
+  do {                                                       \
+    if (maxn == 8) TI_CONTRIB_REG(XT_, ACC_, 8);             \
+    else if (maxn == 16) TI_CONTRIB_REG(XT_, ACC_, 16);      \
+    else TI_CONTRIB_REG(XT_, ACC_, 32);                      \
+  } while (0)
+    if (xdt == TI_F32) {
+      if (f->accum == TI_F64) TI_CONTRIB_REG_N(float, double);
+      else TI_CONTRIB_REG_N(float, float);
+    } else {
+      if (f->accum == TI_F64) TI_CONTRIB_REG_N(double, double);
+      else TI_CONTRIB_REG_N(double, float);
+    }
+#undef TI_CONTRIB_REG_N
+#undef TI_CONTRIB_REG
+    TI_HIP(hipGetLastError());
+    return TI_OK;
+  }
   double* acc = nullptr;
   if (f->accum == TI_F64) {
     acc = static_cast<double*>(out);
@@ -1569,7 +1719,6 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
   }
   TI_HIP(hipMemsetAsync(acc, 0, static_cast<size_t>(rows * W) * 8, stream));
   const size_t lds = static_cast<size_t>(2 * f->shap_maxl + 1) * 64 * 8;
-  const int64_t n_paths = static_cast<int64_t>(d.shap_paths ? 1 : 0) * f->shap_npaths;
   KernelFn fn;
   if (xdt == TI_F32)
     fn = f->accum == TI_F64 ? reinterpret_cast<KernelFn>(contrib_kernel<float, double>)
