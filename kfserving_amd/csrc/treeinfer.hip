@@ -160,15 +160,18 @@ __constant__ ShapInvTable kShapInv = make_inv(std::make_integer_sequence<int, 65
 // or the 1/k table.  The row's contributions accumulate in LDS [W][64]
 // (W = K * (F + 1) <= kShapLdsW), so no global read-modify-write.
 constexpr int kShapLdsW = 128;
+constexpr int64_t kShapWaveTarget = 16384;        // 64-row waves per contrib launch
+constexpr int64_t kShapMinPathsPerSlice = 256;
+constexpr int64_t kShapMaxSlices = 64;
+constexpr uint64_t kShapPartBytesMax = 2ull << 30;
 template <typename XT, typename ACC, int MAXN>
 __global__ void __launch_bounds__(64) contrib_reg_kernel(
     const XT* __restrict__ X, int64_t rows, int64_t stride, int32_t cols, int32_t zero_map_on,
     const ShapPath* __restrict__ paths, int64_t n_paths, const ShapElem* __restrict__ elems,
     const double* __restrict__ leafv, int32_t LW, int32_t K, int32_t F, int32_t maxl,
-    const double* __restrict__ bias, double divisor, double* __restrict__ acc,
-    ACC* __restrict__ out) {
+    const double* __restrict__ bias, double divisor, double* __restrict__ part,
+    int64_t paths_per_slice, ACC* __restrict__ out) {
   (void)maxl;
-  (void)acc;
   extern __shared__ double shap_lds[];
   const int lane = threadIdx.x;
   const int64_t row = (int64_t)blockIdx.x * 64 + lane;
@@ -177,7 +180,9 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
   const int W = K * (F + 1);
   double* phi = shap_lds + lane;                  // phi[j * 64]
   for (int j = 0; j < W; ++j) phi[j * 64] = 0.0;
-  for (int64_t p = 0; p < n_paths; ++p) {
+  const int64_t p_begin = (int64_t)blockIdx.y * paths_per_slice;
+  const int64_t p_end = p_begin + paths_per_slice < n_paths ? p_begin + paths_per_slice : n_paths;
+  for (int64_t p = p_begin; p < p_end; ++p) {
     const ShapPath P = paths[p];
     const int n = P.n;
     const ShapElem* pe = elems + P.first;
@@ -247,9 +252,35 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
     }
   }
   if (!live) return;
+  if (part) {
+    // path slice blockIdx.y: raw partial sums, [slice][W][rows] (coalesced)
+    double* pp = part + (int64_t)blockIdx.y * W * rows + row;
+    for (int j = 0; j < W; ++j) pp[(int64_t)j * rows] = phi[j * 64];
+    return;
+  }
   ACC* o = out + row * W;
   for (int g = 0; g < K; ++g) {
     for (int f = 0; f < F; ++f) o[g * (F + 1) + f] = (ACC)(phi[(g * (F + 1) + f) * 64] / divisor);
+    o[g * (F + 1) + F] = (ACC)bias[g];
+  }
+}
+
+// Sum of the path slices' partials in slice order, / divisor, bias column.
+template <typename ACC>
+__global__ void __launch_bounds__(256) contrib_slices_kernel(
+    const double* __restrict__ part, int32_t slices, int64_t rows, int32_t K, int32_t F,
+    const double* __restrict__ bias, double divisor, ACC* __restrict__ out) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  const int W = K * (F + 1);
+  ACC* o = out + row * W;
+  for (int g = 0; g < K; ++g) {
+    for (int f = 0; f < F; ++f) {
+      const int j = g * (F + 1) + f;
+      double t = 0.0;
+      for (int sl = 0; sl < slices; ++sl) t += part[((int64_t)sl * W + j) * rows + row];
+      o[j] = (ACC)(t / divisor);
+    }
     o[g * (F + 1) + F] = (ACC)bias[g];
   }
 }
@@ -1684,14 +1715,36 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
     const size_t lds_w = static_cast<size_t>(W) * 64 * 8;
     const unsigned grid_r = static_cast<unsigned>((rows + 63) / 64);
     if (rows == 0) return TI_OK;
+    // Path slices: one 64-row wave walks n_paths / slices paths, so a small
+    // batch still fills the 256 CUs (>= kShapWaveTarget waves); partials
+    // [slices][W][rows] are summed in slice order by contrib_slices_kernel.
+    static const int force_slices = env_int("TI_SHAP_SLICES", 0);
+    int64_t slices = force_slices > 0 ? force_slices
+                                      : (kShapWaveTarget + grid_r - 1) / static_cast<int64_t>(grid_r);
+    slices = std::min<int64_t>(slices, std::max<int64_t>(1, n_paths / kShapMinPathsPerSlice));
+    slices = std::min<int64_t>(slices, kShapMaxSlices);
+    while (slices > 1 && static_cast<uint64_t>(slices) * W * rows * 8 > kShapPartBytesMax) --slices;
+    slices = std::max<int64_t>(slices, 1);
+    const int64_t pps = (n_paths + slices - 1) / slices;
+    double* part = nullptr;
+    if (slices > 1)
+      TI_HIP(hipMallocAsync(reinterpret_cast<void**>(&part),
+                            static_cast<size_t>(slices * W * rows) * 8, stream));
 #define TI_CONTRIB_REG(XT_, ACC_, N_)                                                          \
   do {                                                                                         \
     int rc_ = ensure_lds_attr(d.device, reinterpret_cast<KernelFn>(contrib_reg_kernel<XT_, ACC_, N_>)); \
     if (rc_) return rc_;                                                                       \
-    hipLaunchKernelGGL((contrib_reg_kernel<XT_, ACC_, N_>), dim3(grid_r), dim3(64), lds_w, stream, \
+    hipLaunchKernelGGL((contrib_reg_kernel<XT_, ACC_, N_>), dim3(grid_r, (unsigned)slices), dim3(64), \
+                       lds_w, stream,                                                          \
                        static_cast<const XT_*>(X), rows, stride, cols, f->lgb_zero_map,        \
                        d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,    \
-                       f->shap_maxl, d.shap_bias, f->divisor, nullptr, static_cast<ACC_*>(out)); \
+                       f->shap_maxl, d.shap_bias, f->divisor, part, pps, static_cast<ACC_*>(out)); \
+    if (part) {                                                                                \
+      const unsigned g2 = static_cast<unsigned>((rows + 255) / 256);                           \
+      hipLaunchKernelGGL((contrib_slices_kernel<ACC_>), dim3(g2), dim3(256), 0, stream, part,  \
+                         (int32_t)slices, rows, f->K, f->F, d.shap_bias, f->divisor,           \
+                         static_cast<ACC_*>(out));                                             \
+    }                                                                                          \
   } while (0)
 #define TI_CONTRIB_REG_N(XT_, ACC_)                          \
   do {                                                       \
@@ -1709,6 +1762,7 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
 #undef TI_CONTRIB_REG_N
 #undef TI_CONTRIB_REG
     TI_HIP(hipGetLastError());
+    if (part) TI_HIP(hipFreeAsync(part, stream));
     return TI_OK;
   }
   double* acc = nullptr;
