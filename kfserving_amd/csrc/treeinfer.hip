@@ -164,7 +164,7 @@ constexpr int64_t kShapWaveTarget = 16384;        // 64-row waves per contrib la
 constexpr int64_t kShapMinPathsPerSlice = 256;
 constexpr int64_t kShapMaxSlices = 64;
 constexpr uint64_t kShapPartBytesMax = 2ull << 30;
-template <typename XT, typename ACC, int MAXN>
+template <typename XT, typename ACC, typename MT, int MAXN>
 __global__ void __launch_bounds__(64) contrib_reg_kernel(
     const XT* __restrict__ X, int64_t rows, int64_t stride, int32_t cols, int32_t zero_map_on,
     const ShapPath* __restrict__ paths, int64_t n_paths, const ShapElem* __restrict__ elems,
@@ -198,24 +198,24 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
       om |= (follow ? 1u : 0u) << i;
     }
     // ExtendPath from scratch
-    double w[MAXN + 1];
-    w[0] = 1.0;
+    MT w[MAXN + 1];
+    w[0] = MT(1);
 #pragma unroll
     for (int d = 1; d <= MAXN; ++d) {
       if (d <= n) {
-        const double of = ((om >> (d - 1)) & 1u) ? 1.0 : 0.0;
-        const double zf = pe[d - 1].zf;
-        w[d] = 0.0;
+        const MT of = ((om >> (d - 1)) & 1u) ? MT(1) : MT(0);
+        const MT zf = static_cast<MT>(pe[d - 1].zf);
+        w[d] = MT(0);
 #pragma unroll
         for (int i = d - 1; i >= 0; --i) {
-          w[i + 1] += of * w[i] * ((double)(i + 1) / (double)(d + 1));
-          w[i] = zf * w[i] * ((double)(d - i) / (double)(d + 1));
+          w[i + 1] += of * w[i] * static_cast<MT>((double)(i + 1) / (double)(d + 1));
+          w[i] = zf * w[i] * static_cast<MT>((double)(d - i) / (double)(d + 1));
         }
       }
     }
-    const double rn1 = (double)(n + 1);
-    const double in1 = kShapInv.v[n + 1];
-    double wn = 0.0;                              // w[n]
+    const MT rn1 = static_cast<MT>(n + 1);
+    const MT in1 = static_cast<MT>(kShapInv.v[n + 1]);
+    MT wn = MT(0);                              // w[n]
 #pragma unroll
     for (int i = 0; i <= MAXN; ++i)
       if (i == n) wn = w[i];
@@ -224,26 +224,26 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
     for (int e_i = 0; e_i < n; ++e_i) {
       const ShapElem e = pe[e_i];
       const bool one = ((om >> e_i) & 1u) != 0u;
-      const double zf = e.zf;
-      double total = 0.0;
+      const MT zf = static_cast<MT>(e.zf);
+      MT total = MT(0);
       if (one) {
-        double next = wn;
+        MT next = wn;
 #pragma unroll
         for (int i = MAXN - 1; i >= 0; --i) {
           if (i < n) {
-            const double tmp = next * (rn1 * (1.0 / (double)(i + 1)));
+            const MT tmp = next * (rn1 * static_cast<MT>(1.0 / (double)(i + 1)));
             total += tmp;
-            next = w[i] - tmp * zf * ((double)(n - i) * in1);
+            next = w[i] - tmp * zf * (static_cast<MT>(n - i) * in1);
           }
         }
       } else {
-        const double izf = 1.0 / zf;
+        const MT izf = MT(1) / zf;
 #pragma unroll
         for (int i = MAXN - 1; i >= 0; --i) {
-          if (i < n) total += w[i] * izf * (rn1 * kShapInv.v[n - i]);
+          if (i < n) total += w[i] * izf * (rn1 * static_cast<MT>(kShapInv.v[n - i]));
         }
       }
-      const double scale = total * ((one ? 1.0 : 0.0) - zf);
+      const double scale = static_cast<double>(total * ((one ? MT(1) : MT(0)) - zf));
       if (LW == 1) {
         phi[(P.group * (F + 1) + e.feature) * 64] += scale * lv[0];
       } else {
@@ -1730,11 +1730,11 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
     if (slices > 1)
       TI_HIP(hipMallocAsync(reinterpret_cast<void**>(&part),
                             static_cast<size_t>(slices * W * rows) * 8, stream));
-#define TI_CONTRIB_REG(XT_, ACC_, N_)                                                          \
+#define TI_CONTRIB_REG(XT_, ACC_, MT_, N_)                                                          \
   do {                                                                                         \
-    int rc_ = ensure_lds_attr(d.device, reinterpret_cast<KernelFn>(contrib_reg_kernel<XT_, ACC_, N_>)); \
+    int rc_ = ensure_lds_attr(d.device, reinterpret_cast<KernelFn>(contrib_reg_kernel<XT_, ACC_, MT_, N_>)); \
     if (rc_) return rc_;                                                                       \
-    hipLaunchKernelGGL((contrib_reg_kernel<XT_, ACC_, N_>), dim3(grid_r, (unsigned)slices), dim3(64), \
+    hipLaunchKernelGGL((contrib_reg_kernel<XT_, ACC_, MT_, N_>), dim3(grid_r, (unsigned)slices), dim3(64), \
                        lds_w, stream,                                                          \
                        static_cast<const XT_*>(X), rows, stride, cols, f->lgb_zero_map,        \
                        d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,    \
@@ -1746,18 +1746,26 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
                          static_cast<ACC_*>(out));                                             \
     }                                                                                          \
   } while (0)
-#define TI_CONTRIB_REG_N(XT_, ACC_)                          \
+#define TI_CONTRIB_REG_N(XT_, ACC_, MT_)                     \
   do {                                                       \
-    if (maxn == 8) TI_CONTRIB_REG(XT_, ACC_, 8);             \
-    else if (maxn == 16) TI_CONTRIB_REG(XT_, ACC_, 16);      \
-    else TI_CONTRIB_REG(XT_, ACC_, 32);                      \
+    if (maxn == 8) TI_CONTRIB_REG(XT_, ACC_, MT_, 8);        \
+    else if (maxn == 16) TI_CONTRIB_REG(XT_, ACC_, MT_, 16); \
+    else TI_CONTRIB_REG(XT_, ACC_, MT_, 32);                 \
   } while (0)
+    // Path arithmetic in the forest's accumulator type: float64 for LightGBM
+    // and sklearn; float32 for XGBoost, whose TreeShap keeps its path
+    // elements in bst_float (TI_SHAP_F64=1 forces float64).  Contributions
+    // always accumulate in float64.
+    static const int force_f64 = env_int("TI_SHAP_F64", 0);
+    const bool f32_math = f->accum != TI_F64 && !force_f64;
     if (xdt == TI_F32) {
-      if (f->accum == TI_F64) TI_CONTRIB_REG_N(float, double);
-      else TI_CONTRIB_REG_N(float, float);
+      if (f->accum == TI_F64) TI_CONTRIB_REG_N(float, double, double);
+      else if (f32_math) TI_CONTRIB_REG_N(float, float, float);
+      else TI_CONTRIB_REG_N(float, float, double);
     } else {
-      if (f->accum == TI_F64) TI_CONTRIB_REG_N(double, double);
-      else TI_CONTRIB_REG_N(double, float);
+      if (f->accum == TI_F64) TI_CONTRIB_REG_N(double, double, double);
+      else if (f32_math) TI_CONTRIB_REG_N(double, float, float);
+      else TI_CONTRIB_REG_N(double, float, double);
     }
 #undef TI_CONTRIB_REG_N
 #undef TI_CONTRIB_REG
