@@ -178,8 +178,8 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
   const bool live = row < rows;
   const XT* xr = X + (live ? row : rows - 1) * stride;
   const int W = K * (F + 1);
-  double* phi = shap_lds + lane;                  // phi[j * 64]
-  for (int j = 0; j < W; ++j) phi[j * 64] = 0.0;
+  MT* phi = reinterpret_cast<MT*>(shap_lds) + lane;   // phi[j * 64]
+  for (int j = 0; j < W; ++j) phi[j * 64] = MT(0);
   const int64_t p_begin = (int64_t)blockIdx.y * paths_per_slice;
   const int64_t p_end = p_begin + paths_per_slice < n_paths ? p_begin + paths_per_slice : n_paths;
   for (int64_t p = p_begin; p < p_end; ++p) {
@@ -243,11 +243,12 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
           if (i < n) total += w[i] * izf * (rn1 * static_cast<MT>(kShapInv.v[n - i]));
         }
       }
-      const double scale = static_cast<double>(total * ((one ? MT(1) : MT(0)) - zf));
+      const MT scale = total * ((one ? MT(1) : MT(0)) - zf);
       if (LW == 1) {
-        phi[(P.group * (F + 1) + e.feature) * 64] += scale * lv[0];
+        phi[(P.group * (F + 1) + e.feature) * 64] += scale * static_cast<MT>(lv[0]);
       } else {
-        for (int k = 0; k < LW; ++k) phi[(k * (F + 1) + e.feature) * 64] += scale * lv[k];
+        for (int k = 0; k < LW; ++k)
+          phi[(k * (F + 1) + e.feature) * 64] += scale * static_cast<MT>(lv[k]);
       }
     }
   }
@@ -255,12 +256,13 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
   if (part) {
     // path slice blockIdx.y: raw partial sums, [slice][W][rows] (coalesced)
     double* pp = part + (int64_t)blockIdx.y * W * rows + row;
-    for (int j = 0; j < W; ++j) pp[(int64_t)j * rows] = phi[j * 64];
+    for (int j = 0; j < W; ++j) pp[(int64_t)j * rows] = static_cast<double>(phi[j * 64]);
     return;
   }
   ACC* o = out + row * W;
   for (int g = 0; g < K; ++g) {
-    for (int f = 0; f < F; ++f) o[g * (F + 1) + f] = (ACC)(phi[(g * (F + 1) + f) * 64] / divisor);
+    for (int f = 0; f < F; ++f)
+      o[g * (F + 1) + f] = (ACC)(static_cast<double>(phi[(g * (F + 1) + f) * 64]) / divisor);
     o[g * (F + 1) + F] = (ACC)bias[g];
   }
 }
@@ -1712,7 +1714,9 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
   if (W <= kShapLdsW && f->shap_maxl <= 32 && !force_generic) {
     // registers + LDS accumulators: no scratch accumulator, no memset
     const int maxn = f->shap_maxl <= 8 ? 8 : f->shap_maxl <= 16 ? 16 : 32;
-    const size_t lds_w = static_cast<size_t>(W) * 64 * 8;
+    static const int force_f64 = env_int("TI_SHAP_F64", 0);
+    const bool f32_math = f->accum != TI_F64 && !force_f64;
+    const size_t lds_w = static_cast<size_t>(W) * 64 * (f32_math ? 4 : 8);
     const unsigned grid_r = static_cast<unsigned>((rows + 63) / 64);
     if (rows == 0) return TI_OK;
     // Path slices: one 64-row wave walks n_paths / slices paths, so a small
@@ -1754,10 +1758,9 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
   } while (0)
     // Path arithmetic in the forest's accumulator type: float64 for LightGBM
     // and sklearn; float32 for XGBoost, whose TreeShap keeps its path
-    // elements in bst_float (TI_SHAP_F64=1 forces float64).  Contributions
-    // always accumulate in float64.
-    static const int force_f64 = env_int("TI_SHAP_F64", 0);
-    const bool f32_math = f->accum != TI_F64 && !force_f64;
+    // elements and contributions in bst_float (TI_SHAP_F64=1 forces
+    // float64).  Each slice accumulates in that type in LDS (float32 halves
+    // the LDS per workgroup: 2x workgroups per CU); slices sum in float64.
     if (xdt == TI_F32) {
       if (f->accum == TI_F64) TI_CONTRIB_REG_N(float, double, double);
       else if (f32_math) TI_CONTRIB_REG_N(float, float, float);
