@@ -160,7 +160,7 @@ __constant__ ShapInvTable kShapInv = make_inv(std::make_integer_sequence<int, 65
 // or the 1/k table.  The row's contributions accumulate in LDS [W][64]
 // (W = K * (F + 1) <= kShapLdsW), so no global read-modify-write.
 constexpr int kShapLdsW = 128;
-constexpr int64_t kShapWaveTarget = 16384;        // 64-row waves per contrib launch
+constexpr int64_t kShapWaveTarget = 65536;        // 64-row waves per contrib launch (sweep: profiles/r1_shap_sweep.log)
 constexpr int64_t kShapMinPathsPerSlice = 256;
 constexpr int64_t kShapMaxSlices = 64;
 constexpr uint64_t kShapPartBytesMax = 2ull << 30;
