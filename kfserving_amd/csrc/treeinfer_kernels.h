@@ -703,6 +703,22 @@ __device__ __forceinline__ void bheap_stage(const KArgs& a, const unsigned char*
               : "+v"(nd[q]), "+v"(idx[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y)
               : "vcc");
           continue;
+        } else {
+          // NaN tiles: right = (rank < bin) && !(bin == NaN code && NaN-left),
+          // NaN-left being bit 15 = the sign of the node's low half as i16.
+          // 5 VALU (the compiler's form: 9) and two SALU mask ops.
+          uint64_t mn, ml;
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %4 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+              "v_cmp_eq_u32_e64 %2, %7, %4\n\t"
+              "v_cmp_gt_i16_e64 %3, 0, %0\n\t"
+              "s_and_b64 %2, %2, %3\n\t"
+              "s_andn2_b64 vcc, vcc, %2\n\t"
+              "v_cndmask_b32 %0, %5, %6, vcc\n\t"
+              "v_addc_co_u32 %1, vcc, %1, %1, vcc"
+              : "+v"(nd[q]), "+v"(idx[q]), "=&s"(mn), "=&s"(ml)
+              : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y), "s"(BinTraits<B16>::kNan)
+              : "vcc", "scc");
+          continue;
         }
 #endif
         const bool right = !bin_left<B16, CHECK_NAN>(b[q], nd[q]);
