@@ -27,6 +27,7 @@
 #include <string>
 #include <thread>
 #include <utility>
+#include <type_traits>
 #include <vector>
 
 #include "treeinfer.h"
@@ -221,6 +222,47 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
       if (i == n) wn = w[i];
     const double* lv = leafv + P.leaf * LW;
     // UnwoundPathSum per element, times (one - zero) times the leaf value
+    if constexpr (std::is_same<MT, float>::value) {
+      // Two elements at once in packed float32 (v_pk_mul/add_f32), both
+      // branches of the unwind evaluated and selected per lane: the branch
+      // on `one` diverges within a wave anyway.  Same per-element expression
+      // order as the scalar loop below, so the same float results.
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      for (int e_i = 0; e_i < n; e_i += 2) {
+        const bool pair = e_i + 1 < n;
+        const ShapElem ea = pe[e_i];
+        const ShapElem eb = pe[pair ? e_i + 1 : e_i];
+        const bool one_a = ((om >> e_i) & 1u) != 0u;
+        const bool one_b = ((om >> (pair ? e_i + 1 : e_i)) & 1u) != 0u;
+        const f2 zf = {static_cast<float>(ea.zf), static_cast<float>(eb.zf)};
+        const f2 izf = f2{1.0f, 1.0f} / zf;
+        f2 next = {wn, wn};
+        f2 tot1 = {0.0f, 0.0f}, tot0 = {0.0f, 0.0f};
+#pragma unroll
+        for (int i = MAXN - 1; i >= 0; --i) {
+          if (i < n) {
+            const f2 tmp = next * (rn1 * static_cast<float>(1.0 / (double)(i + 1)));
+            tot1 += tmp;
+            next = w[i] - tmp * zf * (static_cast<float>(n - i) * in1);
+            tot0 += w[i] * izf * (rn1 * static_cast<float>(kShapInv.v[n - i]));
+          }
+        }
+        const float sa = (one_a ? tot1.x : tot0.x) * ((one_a ? 1.0f : 0.0f) - zf.x);
+        const float sb = (one_b ? tot1.y : tot0.y) * ((one_b ? 1.0f : 0.0f) - zf.y);
+        if (LW == 1) {
+          const float l0 = static_cast<float>(lv[0]);
+          phi[(P.group * (F + 1) + ea.feature) * 64] += sa * l0;
+          if (pair) phi[(P.group * (F + 1) + eb.feature) * 64] += sb * l0;
+        } else {
+          for (int k = 0; k < LW; ++k) {
+            const float lk = static_cast<float>(lv[k]);
+            phi[(k * (F + 1) + ea.feature) * 64] += sa * lk;
+            if (pair) phi[(k * (F + 1) + eb.feature) * 64] += sb * lk;
+          }
+        }
+      }
+      continue;
+    }
     for (int e_i = 0; e_i < n; ++e_i) {
       const ShapElem e = pe[e_i];
       const bool one = ((om >> e_i) & 1u) != 0u;
