@@ -1743,8 +1743,11 @@ int launch_chunked(ti_forest* f, int slot, const void* X, int xdt, int64_t rows,
   return rc;
 }
 
-// TI_OUTPUT_CONTRIB on one (unchunked) forest: contrib_kernel over the
-// forest's path tables; float32 forests accumulate in a float64 scratch.
+// TI_OUTPUT_CONTRIB on one (unchunked) forest.  contrib_reg_kernel when the
+// row's accumulators fit LDS (K * (F + 1) <= kShapLdsW) and paths have <= 32
+// unique features: path slices over blockIdx.y, partials summed in slice
+// order by contrib_slices_kernel.  Otherwise contrib_kernel, whose float32
+// forests accumulate in a float64 scratch.
 int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows,
                    int32_t cols, int64_t stride, void* out, hipStream_t stream) {
   if (!f->has_shap)
