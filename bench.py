@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 N_TREES, DEPTH, N_FEAT, ROWS = 500, 8, 28, 1_000_000
 HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md)
 LAYOUT_NAMES = {0: "heap", 1: "explicit", 2: "compact", 3: "bheap", 4: "bexplicit",
-                5: "sexplicit"}
+                5: "sexplicit", 6: "rexplicit"}
 
 
 def parse_args():

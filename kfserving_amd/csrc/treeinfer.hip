@@ -418,6 +418,10 @@ struct DeviceForest {
   // binned explicit layout: rank-coded nodes + tables per input dtype
   ExpNode* bx_nodes[2] = {nullptr, nullptr};
   unsigned char* bx_tbl[2] = {nullptr, nullptr};
+  // record explicit layout
+  uint2* rx_recs[2] = {nullptr, nullptr};
+  uint32_t* rx_base = nullptr;
+  uint32_t* rx_nint = nullptr;
   // TreeSHAP path tables
   ShapPath* shap_paths = nullptr;
   ShapElem* shap_elems = nullptr;
@@ -491,6 +495,18 @@ struct ti_forest {
   std::vector<unsigned char> h_sx_vals;
   std::vector<int32_t> h_sx_ids;
   int32_t bx_ilp = 4;               // trees per lane in lockstep (4 or 8)
+  // record explicit layout (6): 8-byte slots per input dtype (ranks differ),
+  // shared per-tree first slot, per-slot leaf values / ids
+  struct RecExplicit {
+    std::vector<uint2> recs;
+    std::vector<unsigned char> tbl;
+    int32_t L = 0;
+    int32_t rows = 256;
+    int32_t words = 0;
+  } rx[2];
+  std::vector<uint32_t> h_rx_base, h_rx_nint;
+  int64_t rx_slots = 0;
+  int32_t rx_ilp = 8;
   std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
   // TreeSHAP (TI_OUTPUT_CONTRIB); has_shap = 0 when the forest has no covers
   int32_t has_shap = 0, shap_maxl = 0;
@@ -533,7 +549,8 @@ void free_device(DeviceForest& d) {
                   d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root, d.cat_words,
                   d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1],
                   d.bx_nodes[0], d.bx_nodes[1], d.bx_tbl[0], d.bx_tbl[1],
-                  d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias};
+                  d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias,
+                  d.rx_recs[0], d.rx_recs[1], d.rx_base, d.rx_nint};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d.hx_pin) (void)hipHostFree(d.hx_pin);
@@ -558,6 +575,8 @@ void free_device(DeviceForest& d) {
     d.bh_img[i] = d.bh_tbl[i] = d.bx_tbl[i] = nullptr;
     d.bx_nodes[i] = nullptr;
   }
+  d.rx_recs[0] = d.rx_recs[1] = nullptr;
+  d.rx_base = d.rx_nint = nullptr;
   d.shap_paths = nullptr;
   d.shap_elems = nullptr;
   d.shap_leaf = d.shap_bias = nullptr;
@@ -1125,6 +1144,116 @@ bool pack_bexplicit(const ti_forest_desc* d, ti_forest* f, ti_forest::BinExplici
   return true;
 }
 
+// ------------------------------------------------ record explicit packing
+// Slots of layout 6 (treeinfer_kernels.h, rx_walk): per tree the internal
+// nodes breadth-first in [0, nint), then the leaves in the same breadth-first
+// order as pack_explicit numbers them (so leaf ids / vector leaves share its
+// tables), n slots for n nodes.  Returns false when a tree has more than
+// 65,535 nodes (16-bit child slots).
+bool plan_rx_slots(const ti_forest_desc* d, ti_forest* f, std::vector<uint32_t>* slot_of) {
+  slot_of->assign(d->n_nodes, 0);
+  f->h_rx_base.assign(d->n_trees, 0);
+  f->h_rx_nint.assign(d->n_trees, 0);
+  if (d->n_nodes >= (int64_t(1) << 31)) return false;
+  std::vector<int32_t> q;
+  for (int t = 0; t < d->n_trees; ++t) {
+    const int64_t b = d->tree_offset[t];
+    const int64_t n = d->tree_offset[t + 1] - b;
+    if (n > 65535) return false;
+    f->h_rx_base[t] = static_cast<uint32_t>(b);   // a tree takes as many slots as nodes
+    q.assign(1, 0);
+    uint32_t n_int = 0;
+    for (size_t qi = 0; qi < q.size(); ++qi) {
+      const int64_t g = b + q[qi];
+      if (d->feature[g] < 0) continue;
+      (*slot_of)[g] = n_int++;
+      q.push_back(d->left[g]);
+      q.push_back(d->right[g]);
+    }
+    uint32_t n_leaf = 0;
+    for (size_t qi = 0; qi < q.size(); ++qi) {
+      const int64_t g = b + q[qi];
+      if (d->feature[g] < 0) (*slot_of)[g] = n_int + n_leaf++;
+    }
+    f->h_rx_nint[t] = n_int;
+  }
+  f->rx_slots = d->n_nodes;
+  return true;
+}
+
+// Records of one input view (ranks differ between the float32 and float64
+// views).  Returns false when the bins do not fit u16 (more than 65,533
+// distinct thresholds on a feature; 16,382 for zero-missing forests, whose
+// bins are doubled) or the bin image does not fit 64 KB at 64-row tiles.
+template <typename XT, typename ACC>
+bool pack_rexplicit(const ti_forest_desc* d, const ti_forest* f,
+                    const std::vector<uint32_t>& slot_of, ti_forest::RecExplicit* rx) {
+  const bool zero = f->zero_rule != 0;
+  const RankTables<XT> rt = collect_ranks<XT>(d, zero);
+  if (rt.m_max > (zero ? 16382u : 65533u)) return false;
+  rx->words = (d->n_features + 1) / 2;
+  int R = env_int("TI_RX_ROWS", 256);
+  while (R > 64 && static_cast<size_t>(rx->words) * R * 4 > kFeatLdsMax) R >>= 1;
+  if (static_cast<size_t>(rx->words) * R * 4 > kFeatLdsMax) return false;
+  rx->rows = R;
+  rx->L = rt.L;
+  eytzinger_tables(rt, &rx->tbl);
+  rx->recs.assign(d->n_nodes, uint2{0u, 0u});
+  const bool scalar_leaves = d->leaf_width == 1;
+  for (int t = 0; t < d->n_trees; ++t) {
+    const int64_t b = d->tree_offset[t];
+    for (int64_t g = b; g < d->tree_offset[t + 1]; ++g) {
+      uint2 r{0u, 0u};
+      if (d->feature[g] < 0) {
+        if (scalar_leaves) {
+          const ACC v = static_cast<ACC>(d->leaf_value[g]);
+          std::memcpy(&r, &v, sizeof(ACC));
+        }
+      } else {
+        const int fe = d->feature[g];
+        const uint32_t off = static_cast<uint32_t>((fe / 2) * R * 4 + (fe % 2) * 2);
+        const uint32_t rank = rt.rank(fe, d->threshold[g]);
+        r.x = off | ((d->flags[g] & TI_NODE_NAN_LEFT) ? ti::kRxNanLeft : 0u);
+        if (zero) {
+          r.x |= (2u * rank + 1u) << 16;
+          if (d->flags[g] & TI_NODE_ZERO_FLIP) r.x |= 0x80000000u;
+        } else {
+          r.x |= rank << 16;
+        }
+        r.y = (slot_of[b + d->right[g]] << 16) | slot_of[b + d->left[g]];
+      }
+      rx->recs[b + slot_of[g]] = r;
+    }
+  }
+  return true;
+}
+
+// Mean depth of the leaves of a forest (every leaf counted once).
+double mean_leaf_depth(const ti_forest_desc* d) {
+  double sum = 0;
+  int64_t n_leaf = 0;
+  std::vector<int32_t> dep, q;
+  for (int t = 0; t < d->n_trees; ++t) {
+    const int64_t b = d->tree_offset[t];
+    const int32_t n = static_cast<int32_t>(d->tree_offset[t + 1] - b);
+    dep.assign(n, 0);
+    q.assign(1, 0);   // breadth-first: a parent's depth is set first
+    for (size_t qi = 0; qi < q.size(); ++qi) {
+      const int32_t v = q[qi];
+      const int64_t g = b + v;
+      if (d->feature[g] < 0) {
+        sum += dep[v];
+        ++n_leaf;
+      } else {
+        dep[d->left[g]] = dep[d->right[g]] = dep[v] + 1;
+        q.push_back(d->left[g]);
+        q.push_back(d->right[g]);
+      }
+    }
+  }
+  return n_leaf ? sum / n_leaf : 0.0;
+}
+
 // TreeSHAP path tables + bias (see ShapPath).  Forests without covers or
 // with categorical splits get none (TI_OUTPUT_CONTRIB is then unsupported).
 struct ShapBuilder {
@@ -1246,6 +1375,20 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
     if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
     d.leaves = lv;
     if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
+  } else if (f->layout == 6) {
+    for (int i = 0; i < 2; ++i) {
+      if ((rc = upload(&d.rx_recs[i], f->rx[i].recs, &d.bytes))) return rc;
+      if ((rc = upload(&d.bx_tbl[i], f->rx[i].tbl, &d.bytes))) return rc;
+    }
+    if ((rc = upload(&d.rx_base, f->h_rx_base, &d.bytes))) return rc;
+    if ((rc = upload(&d.rx_nint, f->h_rx_nint, &d.bytes))) return rc;
+    if ((rc = upload(&d.leaf_base, f->h_leaf_base, &d.bytes))) return rc;
+    if (f->LW > 1) {   // vector leaves are read from the leaf table
+      unsigned char* lv = nullptr;
+      if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
+      d.leaves = lv;
+    }
+    if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
   } else if (f->layout == 5) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.bh_img[i], f->bx[i].sx, &d.bytes))) return rc;
@@ -1313,6 +1456,13 @@ KernelFn select_bexplicit(int xdt, int accum, int K, bool b16, bool z, int ilp) 
   return ti::kernels_df(4, K, true, z, b16, ilp);
 }
 
+KernelFn select_rexplicit(int xdt, int accum, int K, bool z, int ilp) {
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(6, K, true, z, true, ilp);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(6, K, true, z, true, ilp);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(6, K, true, z, true, ilp);
+  return ti::kernels_df(6, K, true, z, true, ilp);
+}
+
 KernelFn select_sexplicit(int xdt, int accum, int K, bool b16, bool z, int ilp) {
   if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(5, K, true, z, b16, ilp);
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(5, K, true, z, b16, ilp);
@@ -1371,6 +1521,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     R = f->bh[xdt == TI_F64 ? 1 : 0].rows;
   } else if (f->layout == 4 || f->layout == 5) {
     R = f->bx[xdt == TI_F64 ? 1 : 0].rows;
+  } else if (f->layout == 6) {
+    R = f->rx[xdt == TI_F64 ? 1 : 0].rows;
   } else {
     R = 256;
     while (R > 64 && static_cast<size_t>(f->F) * R * xs > kFeatLdsMax) R >>= 1;
@@ -1382,6 +1534,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   if (f->layout == 3) feat_bytes = static_cast<size_t>(f->bh[xdt == TI_F64 ? 1 : 0].words) * R * 4;
   if (f->layout == 4 || f->layout == 5)
     feat_bytes = static_cast<size_t>(f->bx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
+  if (f->layout == 6) feat_bytes = static_cast<size_t>(f->rx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
 
   KArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1495,6 +1648,28 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.bin_words = bx.words;
     lds = feat_bytes + 16;
     KernelFn fn = select_bexplicit(xdt, f->accum, f->K, bx.b16 != 0, f->zero_rule != 0, f->bx_ilp);
+    int rc = ensure_lds_attr(d.device, fn);
+    if (rc) return rc;
+    const int64_t grid = (rows + R - 1) / R;
+    if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    TI_HIP(hipGetLastError());
+    return TI_OK;
+  } else if (f->layout == 6) {
+    const int ii = xdt == TI_F64 ? 1 : 0;
+    const ti_forest::RecExplicit& rx = f->rx[ii];
+    a.rx_recs = d.rx_recs[ii];
+    a.rx_base = d.rx_base;
+    a.rx_nint = d.rx_nint;
+    a.leaf_base = d.leaf_base;
+    a.rx_slots = static_cast<uint32_t>(f->rx_slots);
+    a.leaves = d.leaves;
+    a.exp_leaf_ids = d.exp_leaf_ids;
+    a.bin_tbl = d.bx_tbl[ii];
+    a.bin_L = rx.L;
+    a.bin_words = rx.words;
+    lds = feat_bytes + 16;
+    KernelFn fn = select_rexplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->rx_ilp);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -2037,7 +2212,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   bool use_compact = false;
   if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
   if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
-  if (want == "explicit" || want == "bexplicit" || want == "sexplicit") {
+  if (want == "explicit" || want == "bexplicit" || want == "sexplicit" || want == "rexplicit") {
     use_heap = false;
     use_compact = false;
   }
@@ -2103,9 +2278,38 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
       pack_explicit<double>(desc, f.get(), false);
     else
       pack_explicit<float>(desc, f.get(), false);
+    // record explicit slots (layout 6) unless a categorical split needs raw
+    // values or another explicit kernel is forced
+    bool rx_ok = false;
+    if (!f->has_cat && want != "explicit" && want != "bexplicit" && want != "sexplicit" &&
+        env_int("TI_NO_REXPLICIT", 0) == 0) {
+      std::vector<uint32_t> slot_of;
+      rx_ok = plan_rx_slots(desc, f.get(), &slot_of);
+      if (rx_ok && f->accum == TI_F64)
+        rx_ok = pack_rexplicit<float, double>(desc, f.get(), slot_of, &f->rx[0]) &&
+                pack_rexplicit<double, double>(desc, f.get(), slot_of, &f->rx[1]);
+      else if (rx_ok)
+        rx_ok = pack_rexplicit<float, float>(desc, f.get(), slot_of, &f->rx[0]) &&
+                pack_rexplicit<double, float>(desc, f.get(), slot_of, &f->rx[1]);
+      if (rx_ok) {
+        f->layout = 6;
+        // trees in flight per lane: 16 for shallow-on-average forests (C3,
+        // mean leaf depth ~9: 7.70 ms vs 7.79 at 8), 8 for deep ones (C4,
+        // sklearn depth 16: 3.06 ms vs 3.13 at 16); profiles/r2_rx_sweep.jsonl
+        const double md = mean_leaf_depth(desc);
+        f->rx_ilp = md < 12.0 ? 16 : 8;
+        const int force_ilp = env_int("TI_RX_ILP", 0);
+        if (force_ilp > 0) f->rx_ilp = force_ilp >= 16 ? 16 : force_ilp >= 8 ? 8 : 4;
+      } else {
+        for (auto& rx : f->rx) rx = ti_forest::RecExplicit();
+        f->h_rx_base.clear();
+        f->h_rx_nint.clear();
+        f->rx_slots = 0;
+      }
+    }
     // rank-binned explicit nodes unless a categorical split needs raw values
     // (TI_FORCE_LAYOUT=explicit keeps the float-compare kernel)
-    if (!f->has_cat && want != "explicit" && env_int("TI_NO_BEXPLICIT", 0) == 0) {
+    if (!rx_ok && !f->has_cat && want != "explicit" && env_int("TI_NO_BEXPLICIT", 0) == 0) {
       // the LDS-staged walk (layout 5) is opt-in: at C3's F = 100 the stage costs
       // the third workgroup per CU and the walk runs 0.65x layout 4
       if (want == "sexplicit") plan_slots(desc, f.get());
@@ -2117,28 +2321,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         // to cover the L2 latency (measured 8.97 vs 10.8 ms at 4); deep
         // balanced forests (sklearn depth 16, C4) are faster at 4 (3.46 vs
         // 3.61 ms at 8), where a group's deepest path costs more.
-        double sum = 0;
-        int64_t n_leaf = 0;
-        std::vector<int32_t> dep;
-        for (int t = 0; t < desc->n_trees; ++t) {
-          const int64_t b = desc->tree_offset[t];
-          const int32_t n = static_cast<int32_t>(desc->tree_offset[t + 1] - b);
-          dep.assign(n, 0);
-          std::vector<int32_t> q(1, 0);   // breadth-first: a parent's depth is set first
-          for (size_t qi = 0; qi < q.size(); ++qi) {
-            const int32_t v = q[qi];
-            const int64_t g = b + v;
-            if (desc->feature[g] < 0) {
-              sum += dep[v];
-              ++n_leaf;
-            } else {
-              dep[desc->left[g]] = dep[desc->right[g]] = dep[v] + 1;
-              q.push_back(desc->left[g]);
-              q.push_back(desc->right[g]);
-            }
-          }
-        }
-        const double mean_depth = n_leaf ? sum / n_leaf : 0.0;
+        const double mean_depth = mean_leaf_depth(desc);
         f->bx_ilp = mean_depth < 12.0 ? 8 : 4;
         const int force_ilp = env_int("TI_BEXP_ILP", 0);
         if (force_ilp > 0) f->bx_ilp = force_ilp >= 8 ? 8 : 4;
@@ -2187,6 +2370,14 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   }
   f->h_exp_src.clear();
   f->h_exp_src.shrink_to_fit();
+  for (auto& rx : f->rx) {
+    rx.recs.clear();
+    rx.recs.shrink_to_fit();
+    rx.tbl.clear();
+    rx.tbl.shrink_to_fit();
+  }
+  f->h_rx_base.clear(); f->h_rx_base.shrink_to_fit();
+  f->h_rx_nint.clear(); f->h_rx_nint.shrink_to_fit();
   f->h_paths.clear();
   f->h_paths.shrink_to_fit();
   f->h_elems.clear();

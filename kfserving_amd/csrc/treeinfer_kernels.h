@@ -116,6 +116,11 @@ struct KArgs {
   int32_t bin_words;              // packed bin words per row (C)
   int32_t bin_chunk;              // columns binned per pass through the temp area
   int32_t stage_off;              // LDS byte offset of the tree stage / temp area
+  // record explicit layout (6): 8-byte slots, first slot of each tree
+  const uint2* rx_recs;           // [slots]
+  const uint32_t* rx_base;        // [T] first slot of each tree
+  const uint32_t* rx_nint;        // [T] internal slots of each tree (leaves follow)
+  uint32_t rx_slots;              // slots in rx_recs
   // shared
   const int32_t* tree_group;      // [T]
   void* out;
@@ -1213,6 +1218,280 @@ __global__ void __launch_bounds__(256) sexplicit_predict_kernel(const KArgs a) {
     else
       sx_stage<ACC, KMAX, B16, ZERO, false, ILP>(a, cnt, t0, acc, lane_off, row, live);
   }
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
+// ---- record explicit (layout 6) --------------------------------------------
+// Deep / irregular trees (LightGBM leaf-wise C3, sklearn depth 16 C4).  What
+// bounds a walk whose nodes come from L2 is the vector-memory pipe, not the
+// ALU: the PMC pass of the binned explicit kernel (layout 4, 16-byte nodes,
+// profiles/r2_c3_l4_pmc.json) has the TD busy ~93 % of the kernel and the TA
+// ~77 %, i.e. the cost is the number of 64-byte requests a wave's gather
+// makes (one per distinct sector within each group of lanes the TA takes per
+// cycle: 4 lanes for 16-byte loads, 8 for 8-byte).  So this layout
+//   * uses 8-byte records (twice the lanes per TA cycle, twice the nodes per
+//     sector);
+//   * masks the gathers of lanes already at a leaf (a finished lane makes no
+//     request; a tree whose 64 lanes are all done costs the wave nothing);
+//   * keeps the leaf value in the leaf's own record, so reaching the leaf is
+//     the last gather of the tree (layout 4 gathers the value again).
+// A tree is a block of slots: internal nodes [0, nint) breadth-first, then the
+// leaves [nint, nslots).  Internal record:
+//   x = rank << 16 | bin byte offset (lane-free part, even: u16 bins) | NaN-left
+//   y = right slot << 16 | left slot
+// Leaf record: the leaf value (ACC: float in x, or double in x:y) when leaves
+// are scalars; leaf ids and vector leaves are found from the slot (leaf index =
+// the tree's first leaf + slot - nint).  Split rule on bins:
+//   right = (rank < b) ^ (b == kNan && NaN-left)
+// LightGBM zero-missing forests (ZERO) bin as b2 = 2 b + (x == 0) with NaN =
+// 0xFFFE and store rank2 = 2 rank + 1 (rank2 < b2 <=> rank < b, exactly) and
+// the zero flip in x bit 31:  right ^= (b2 odd) && zero-flip.
+constexpr uint32_t kRxNanLeft = 1u;
+
+// Slot loads are structured buffer loads: vindex = the slot (VGPR), soffset =
+// the tree's first byte (wave-uniform SGPR), stride 8 in the resource, so the
+// slot -> address step costs no VALU (buffer_load_dwordx2 ... idxen).
+typedef int rx_rsrc_t __attribute__((ext_vector_type(4)));
+typedef unsigned rx_u2_t __attribute__((ext_vector_type(2)));
+__device__ rx_u2_t rx_struct_load(rx_rsrc_t rsrc, uint32_t vindex, uint32_t voffset,
+                                  uint32_t soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.load.v2i32");
+
+__device__ __forceinline__ rx_rsrc_t rx_make_rsrc(const void* base, uint32_t n_slots) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  rx_rsrc_t r;
+  r.x = static_cast<int>(static_cast<uint32_t>(a));
+  r.y = static_cast<int>(static_cast<uint32_t>(a >> 32) | (8u << 16));   // stride 8 B
+  r.z = static_cast<int>(n_slots);                                         // records (slots)
+  r.w = 0x00020000;                                                        // 32-bit data format
+  return r;
+}
+
+// One split decision, hand-scheduled: the rank compare on the record's high
+// half, the flips, then the child slot picked from the two halves of y by
+// one SDWA select on the compare's mask.
+template <bool ZERO, bool CHECK_NAN>
+__device__ __forceinline__ uint32_t rx_next(uint32_t x, uint32_t y, uint32_t b) {
+  uint32_t slot;
+  if (!ZERO && !CHECK_NAN) {
+    asm("v_cmp_lt_u32_sdwa vcc, %1, %3 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_cndmask_b32_sdwa %0, %2, %2, vcc src0_sel:WORD_0 src1_sel:WORD_1"
+        : "=v"(slot) : "v"(x), "v"(y), "v"(b) : "vcc");
+  } else if (!ZERO) {
+    uint64_t n, m;
+    uint32_t t;
+    asm("v_cmp_lt_u32_sdwa vcc, %4, %6 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_cmp_eq_u32_e64 %1, %7, %6\n\t"
+        "v_and_b32 %3, 1, %4\n\t"
+        "v_cmp_ne_u32_e64 %2, 0, %3\n\t"
+        "s_and_b64 %1, %1, %2\n\t"
+        "s_xor_b64 vcc, vcc, %1\n\t"
+        "v_cndmask_b32_sdwa %0, %5, %5, vcc src0_sel:WORD_0 src1_sel:WORD_1"
+        : "=v"(slot), "=&s"(n), "=&s"(m), "=&v"(t)
+        : "v"(x), "v"(y), "v"(b), "s"(0xFFFFu)
+        : "vcc", "scc");
+  } else {
+    // rank2 = x bits 16..30; zero flip = x bit 31 (x < 0 as i32); b2 odd = exact 0
+    uint64_t z, w, n, m;
+    uint32_t r, t;
+    if (!CHECK_NAN) {
+      asm("v_bfe_u32 %3, %5, 16, 15\n\t"
+          "v_cmp_lt_u32_e32 vcc, %3, %7\n\t"
+          "v_and_b32 %4, 1, %7\n\t"
+          "v_cmp_ne_u32_e64 %1, 0, %4\n\t"
+          "v_cmp_gt_i32_e64 %2, 0, %5\n\t"
+          "s_and_b64 %1, %1, %2\n\t"
+          "s_xor_b64 vcc, vcc, %1\n\t"
+          "v_cndmask_b32_sdwa %0, %6, %6, vcc src0_sel:WORD_0 src1_sel:WORD_1"
+          : "=v"(slot), "=&s"(z), "=&s"(w), "=&v"(r), "=&v"(t)
+          : "v"(x), "v"(y), "v"(b)
+          : "vcc", "scc");
+    } else {
+      asm("v_bfe_u32 %5, %7, 16, 15\n\t"
+          "v_cmp_lt_u32_e32 vcc, %5, %9\n\t"
+          "v_and_b32 %6, 1, %9\n\t"
+          "v_cmp_ne_u32_e64 %1, 0, %6\n\t"
+          "v_cmp_gt_i32_e64 %2, 0, %7\n\t"
+          "s_and_b64 %1, %1, %2\n\t"
+          "s_xor_b64 vcc, vcc, %1\n\t"
+          "v_cmp_eq_u32_e64 %3, %10, %9\n\t"
+          "v_and_b32 %6, 1, %7\n\t"
+          "v_cmp_ne_u32_e64 %4, 0, %6\n\t"
+          "s_and_b64 %3, %3, %4\n\t"
+          "s_xor_b64 vcc, vcc, %3\n\t"
+          "v_cndmask_b32_sdwa %0, %8, %8, vcc src0_sel:WORD_0 src1_sel:WORD_1"
+          : "=v"(slot), "=&s"(z), "=&s"(w), "=&s"(n), "=&s"(m), "=&v"(r), "=&v"(t)
+          : "v"(x), "v"(y), "v"(b), "s"(0xFFFEu)
+          : "vcc", "scc");
+    }
+  }
+  return slot;
+}
+
+// Bin the tile's rows (as stage_bins_rows, one lane per row, per-lane loads)
+// into the u16 image of layout 6: b = 1 + #{u < x}, NaN = 0xFFFF; with ZB
+// (zero-missing forests) b2 = 2 b + (x == 0) and NaN = 0xFFFE.
+template <typename XT, bool ZB>
+__device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
+                                              int R, int tid) {
+  constexpr int Q = 8;
+  const XT* tbl = static_cast<const XT*>(a.bin_tbl);
+  const int F = a.n_features;
+  const int FC = F < a.n_cols ? F : a.n_cols;
+  const int L = a.bin_L;
+  const uint32_t tsz = 1u << L;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  const XT* xr = static_cast<const XT*>(a.X) + (live ? row : a.n_rows - 1) * a.row_stride;
+  bool has_nan = false;
+  if (tid == 0) *flag = 0;
+  for (int f0 = 0; f0 < F; f0 += Q) {
+    XT x[Q];
+    const XT* tq[Q];
+    uint32_t k[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int f = f0 + q < F ? f0 + q : F - 1;
+      x[q] = f0 + q < FC ? zero_map(xr[f], a.lgb_zero_map) : nan_value<XT>();
+      tq[q] = tbl + (size_t)f * tsz;
+      k[q] = 1u;
+    }
+    for (int s = 0; s < L; ++s) {
+      XT e[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) e[q] = tq[q][k[q]];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
+    }
+    uint32_t w[Q / 2];
+#pragma unroll
+    for (int j = 0; j < Q / 2; ++j) w[j] = 0u;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const bool nan = x[q] != x[q];
+      has_nan |= nan && (f0 + q < F);
+      uint32_t b = 1u + k[q] - tsz;
+      if (ZB) b = nan ? 0xFFFEu : 2u * b + (x[q] == XT(0) ? 1u : 0u);
+      else b = nan ? 0xFFFFu : b;
+      w[q / 2] |= b << ((q % 2) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < Q / 2; ++j) {
+      const int word = f0 / 2 + j;
+      if (word < a.bin_words) {
+        __attribute__((address_space(3))) uint32_t* dst =
+            reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+                static_cast<uintptr_t>((uint32_t)(word * R + tid) * 4u));
+        *dst = w[j];
+      }
+    }
+  }
+  __syncthreads();   // flag = 0 is visible before any lane sets it
+  if (has_nan && live) *flag = 1;
+  __syncthreads();
+  return *flag != 0;
+}
+
+// Per step every tree's bin read is issued first, then each tree's decision
+// and its exec-masked gather: only lanes still inside the tree gather, so a
+// finished lane makes no request and keeps its record -- the leaf's value,
+// read by the gather that reached it.  The gathers carry no control flow
+// around them, so the compiler's counted waits keep all ILP in flight.
+template <typename ACC, int KMAX, bool ZERO, bool CHECK_NAN, int ILP>
+__device__ __forceinline__ void rx_walk(const KArgs& a, ACC (&acc)[KMAX], uint32_t lane_off,
+                                        int64_t row, bool live) {
+  const int T = a.n_trees;
+  const int LW = a.leaf_width;
+  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
+  const bool value_in_slot = LW == 1 && !want_leaf;
+  const rx_rsrc_t rsrc = rx_make_rsrc(a.rx_recs, a.rx_slots);
+  const uint32_t bin_limit = (uint32_t)a.bin_words * blockDim.x * 4u;
+  // read-only tables addressed by wave-uniform indices: the constant address
+  // space makes these scalar loads
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  cu32* rx_base = reinterpret_cast<cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  cu32* rx_nint = reinterpret_cast<cu32*>(reinterpret_cast<uintptr_t>(a.rx_nint));
+  for (int t0 = 0; t0 < T; t0 += ILP) {
+    uint32_t sb[ILP], ni[ILP];   // tree's first byte and internal-slot count (SGPRs)
+    uint32_t slot[ILP];          // the lane's slot in each tree
+    rx_u2_t rec[ILP];            // the record gathered last
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = (t0 + q) < T ? (t0 + q) : (T - 1);
+      sb[q] = rx_base[tq] << 3;
+      ni[q] = rx_nint[tq];
+      slot[q] = 0u;
+      rec[q] = rx_struct_load(rsrc, 0u, 0u, sb[q], 0);   // the root (or a lone leaf)
+    }
+    for (;;) {
+      bool any = false;
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) any |= slot[q] < ni[q];
+      if (__ballot(any) == 0) break;   // every lane of every tree at a leaf
+      // bins: a lane at its leaf (record = the value) reads a clamped, harmless
+      // address; the image ends at bin_limit
+      uint32_t b[ILP];
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        const uint32_t ad = (rec[q].x & 0xFFFEu) | lane_off;
+        b[q] = lds_bin<true>(ad < bin_limit ? ad : lane_off);
+      }
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        const bool in = slot[q] < ni[q];
+        const uint32_t nx = rx_next<ZERO, CHECK_NAN>(rec[q].x, rec[q].y, b[q]);
+        slot[q] = in ? nx : slot[q];
+        // only lanes still inside the tree gather (exec-masked: a finished
+        // lane makes no request and keeps its record, the leaf value)
+        if (in) rec[q] = rx_struct_load(rsrc, nx, 0u, sb[q], 0);
+      }
+    }
+    if (value_in_slot) {
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        if (t0 + q < T) {
+          ACC v;
+          if (sizeof(ACC) == 8) v = (ACC)__hiloint2double((int)rec[q].y, (int)rec[q].x);
+          else v = (ACC)__uint_as_float(rec[q].x);
+          add_leaf<ACC, KMAX>(acc, &v, 0, 1, a.tree_group[t0 + q]);
+        }
+      }
+    } else {
+      // leaf ids / vector leaves: the leaf's index from its slot
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        if (t0 + q < T) {
+          const int64_t li = a.leaf_base[t0 + q] + (int64_t)(slot[q] - ni[q]);
+          if (want_leaf) {
+            if (live) static_cast<int32_t*>(a.out)[row * T + t0 + q] = a.exp_leaf_ids[li];
+          } else {
+            add_leaf<ACC, KMAX>(acc, static_cast<const ACC*>(a.leaves) + li * LW, 0, LW,
+                                a.tree_group[t0 + q]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
+__global__ void __launch_bounds__(256) rexplicit_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  const bool tile_nan = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid);
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  ACC acc[KMAX];
+  init_acc(acc, a);
+  if (tile_nan)
+    rx_walk<ACC, KMAX, ZERO, true, ILP>(a, acc, lane_off, row, live);
+  else
+    rx_walk<ACC, KMAX, ZERO, false, ILP>(a, acc, lane_off, row, live);
   if (!live || a.kind == TI_OUTPUT_LEAF) return;
   finish_row<ACC, KMAX>(acc, a, row);
 }

@@ -185,7 +185,7 @@ def test_sklearn_goldens_bit_exact(golden):
     f = load_tree_arrays(os.path.join(golden, "sk_rf_reg_model.npz"))
     g = np.load(os.path.join(golden, "sk_rf_reg.npz"))
     dev = DeviceForest(f, [0])
-    assert dev.info()["layout"] in (1, 4)     # depth-16 trees: (binned) explicit layout
+    assert dev.info()["layout"] in (1, 4, 6)   # depth-16 trees: an explicit layout
     assert np.array_equal(dev.predict(g["X"], OUT_PREDICT), g["predict"])
     assert np.array_equal(dev.predict(g["X"], OUT_LEAF), g["apply"])
     fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
@@ -340,11 +340,12 @@ def _dev_with_layout(forest, layout):
             os.environ["TI_FORCE_LAYOUT"] = old
 
 
-LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2, "bheap": 3, "bexplicit": 4, "sexplicit": 5}
+LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2, "bheap": 3, "bexplicit": 4, "sexplicit": 5,
+             "rexplicit": 6}
 
 
 @pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit"])
+                                    "sexplicit", "rexplicit"])
 def test_xgb_golden_every_layout(golden, layout):
     g = np.load(os.path.join(golden, "xgb_synth.npz"))
     trees, ti = xf.synthetic_complete_trees(40, 8, 28, seed=1)
@@ -360,7 +361,7 @@ def test_xgb_golden_every_layout(golden, layout):
     np.testing.assert_allclose(dev3.predict(g["X"], OUT_PREDICT), g["prob3"], rtol=RTOL)
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit"])
+@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
     g = np.load(os.path.join(golden, "lgb_synth.npz"))
@@ -378,7 +379,7 @@ def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
 
 
 @pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit"])
+                                    "sexplicit", "rexplicit"])
 def test_lgb_iris_fixture_every_layout(golden, layout):
     from sklearn.datasets import load_iris
     path = os.path.join(golden, "lgb_iris_v3.txt")
@@ -388,7 +389,7 @@ def test_lgb_iris_fixture_every_layout(golden, layout):
     assert np.array_equal(dev.predict(X, OUT_MARGIN), lgb_ref.predict(m, X, raw_score=True))
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit"])
+@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit"])
 def test_sklearn_classifier_every_layout(golden, layout):
     fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
     gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
@@ -420,7 +421,7 @@ def test_compact_ragged_and_specials(rows):
                           port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
 
 
-@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit"])
+@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit", "rexplicit"])
 @pytest.mark.parametrize("rows", [1, 255, 257, 3000])
 def test_bexplicit_zero_missing_and_specials(rows, layout):
     """Binned explicit kernels (nodes in global memory / staged in LDS) on
