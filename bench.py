@@ -9,14 +9,23 @@ collective ("weak": every rank predicts its own 1M rows); value = all ranks'
 rows / max-over-ranks wall time.
 
 Also reported (rank 0):
-  roofline     -- SURVEY.md 8(d) byte model per launch: B_visit = 8 B x V + 4 B x F
-                  + 4 B out, V = node visits per row (500 x 8 = 4000), divided by
-                  the kernel's average duration measured with HIP events on the
-                  launch stream; traffic = HBM bytes from a committed rocprofv3 PMC
-                  pass (profiles/), or null.
+  roofline     -- the resource that binds the C2 kernel: VALU issue (DESIGN.md
+                  4).  achieved = VALU wave-instructions per launch (committed
+                  rocprofv3 PMC pass of the same kernel, profiles/pmc_c2.json)
+                  / the kernel's average duration from HIP events on the launch
+                  stream; peak = 1,024 SIMDs x 2.4 GHz / 4 cycles per wave64
+                  VALU instruction.  The HBM view is kept beside it:
+                  compulsory bytes (X + out) and counter bytes (FETCH_SIZE +
+                  WRITE_SIZE) per launch as fractions of 8 TB/s.
   cpu_baseline -- the C/OpenMP restatement of xgboost 0.82's predict loop
                   (oracle/c/tree_port.c, kind "port": xgboost is not installed)
                   timed on this host on a bounded sample of the same rows.
+  c3, c4       -- the other named GPU configs at their BASELINE sizes, row-
+                  sharded over the ranks (strong scaling, max-over-ranks wall):
+                  C3 LightGBM leaf-wise 1000 x 255 leaves, F = 100, 100M rows;
+                  C4 sklearn RandomForestRegressor 200 x depth 16, F = 64, 10M
+                  rows (the cached fit of scripts/make_c4_model.py).
+  batched_latency, nan_variant -- see the functions below.
 """
 from __future__ import annotations
 
@@ -33,11 +42,13 @@ sys.path.insert(0, ROOT)
 
 N_TREES, DEPTH, N_FEAT, ROWS = 500, 8, 28, 1_000_000
 HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md)
+SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 4.0
+VALU_PEAK = SIMDS * CLOCK_HZ / VALU_CYCLES     # wave64 VALU instructions / s
 LAYOUT_NAMES = {0: "heap", 1: "explicit", 2: "compact", 3: "bheap", 4: "bexplicit",
                 5: "sexplicit", 6: "rexplicit"}
 
 
-def parse_args():
+def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -52,8 +63,13 @@ def parse_args():
     p.add_argument("--latency-qps", type=float, default=10000.0,
                    help="offered requests/s for the batched-latency leg (0 = skip)")
     p.add_argument("--latency-seconds", type=float, default=3.0)
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
-    return p.parse_args()
+    p.add_argument("--configs", default="c3,c4",
+                   help="other named configs to time after the headline ('' = none)")
+    p.add_argument("--rows3", type=int, default=100_000_000)
+    p.add_argument("--rows4", type=int, default=10_000_000)
+    p.add_argument("--config-steps", type=int, default=2)
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
+    return p.parse_args(argv)
 
 
 def build_model():
@@ -71,6 +87,13 @@ def shard_rows(total_rows: int, rank: int, world: int):
     return total_rows, 1000 + rank
 
 
+def strong_shard(total: int, rank: int, world: int):
+    """Strong scaling (C3 / C4): contiguous row blocks of one batch."""
+    per = (total + world - 1) // world
+    lo = min(total, rank * per)
+    return lo, min(total, lo + per)
+
+
 def max_over_ranks(value: float, device) -> float:
     """The slowest rank's wall time (the only collective, outside the timed region)."""
     import torch
@@ -80,6 +103,32 @@ def max_over_ranks(value: float, device) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def barrier_sync(dev_sync):
+    import torch.distributed as dist
+    dev_sync()
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()
+    dev_sync()
+
+
+def timed_steps(step, steps, dev_sync, events=None):
+    """K steps bracketed by barrier + device sync on both sides; returns the
+    wall time and (with `events` = (start, end) timing events recorded on the
+    launch stream) the event time per step in ms."""
+    barrier_sync(dev_sync)
+    t0 = time.perf_counter()
+    if events:
+        events[0].record()
+    for _ in range(steps):
+        step()
+    if events:
+        events[1].record()
+    barrier_sync(dev_sync)
+    wall = time.perf_counter() - t0
+    ev_ms = events[0].elapsed_time(events[1]) / steps if events else None
+    return wall, ev_ms
 
 
 def cpu_baseline(trees, ti, X_host, target_s):
@@ -97,6 +146,40 @@ def cpu_baseline(trees, ti, X_host, target_s):
             "sample": f"{n} rows of the same 1M x 28 batch, oracle/c/tree_port.c "
                       f"(xgboost 0.82 predict loop restated, OpenMP {n_thr} threads), "
                       f"{dt:.1f} s"}
+
+
+def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str):
+    """Binding-resource roofline of the C2 kernel (see the module docstring)."""
+    pmc = None
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as fh:
+                pmc = json.load(fh)
+        except (OSError, ValueError):
+            pmc = None
+    if pmc and not (pmc.get("rows") == rows and pmc.get("workload") == "c2"
+                    and pmc.get("layout") == layout and "valu_insts_per_launch" in pmc):
+        pmc = None       # a pass of another kernel / size does not describe this one
+    t = kernel_ms * 1e-3
+    compulsory = (4 * N_FEAT + 4) * rows
+    out = {"bound": "valu_issue", "unit": "Ginst/s", "peak": VALU_PEAK / 1e9,
+           "achieved": None, "frac": None, "traffic": None, "kernel_ms": kernel_ms,
+           "peak_basis": f"{SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz / {VALU_CYCLES:g} cycles per "
+                         "wave64 VALU instruction",
+           "hbm_compulsory_bytes": compulsory,
+           "hbm_compulsory_frac": compulsory / t / HBM_PEAK}
+    if pmc:
+        valu = pmc["valu_insts_per_launch"]
+        out["achieved"] = valu / t / 1e9
+        out["frac"] = valu / t / VALU_PEAK
+        out["valu_insts_per_launch"] = valu
+        out["traffic"] = pmc.get("hbm_bytes_per_launch")
+        if out["traffic"]:
+            out["hbm_counter_frac"] = out["traffic"] / t / HBM_PEAK
+            out["traffic_over_compulsory"] = out["traffic"] / (compulsory + pmc.get(
+                "model_bytes", 0))
+        out["pmc_source"] = pmc.get("source")
+    return out
 
 
 def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5, seed=7,
@@ -128,7 +211,7 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
         batch_ms.append((time.perf_counter() - t) * 1e3)
         return {"predictions": out}
 
-    async def run():
+    async def run_load():
         b = Batcher(predict_batch, max_batch_size=max_batch, max_latency_ms=max_latency_ms)
         loop = asyncio.get_running_loop()
         t0 = loop.time() + 0.05
@@ -154,7 +237,7 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
         from kfserving_amd.kfserving.kfserver import tune_gc
         tune_gc()
     try:
-        wall = asyncio.run(run())
+        wall = asyncio.run(run_load())
     finally:
         if freeze_gc:
             gc.unfreeze()
@@ -172,30 +255,145 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
             "path": "in-process batcher -> ti_predict (host buffers), 1 GPU, no HTTP/JSON"}
 
 
-def main():
-    args = parse_args()
+# ------------------------------------------------------------ other configs
+def device_normal(rows, cols, seed, device):
+    """X ~ N(0,1) float32 generated on the device in 8M-row chunks (seed, chunk)."""
+    import torch
+    X = torch.empty((rows, cols), dtype=torch.float32, device=device)
+    chunk = 8 << 20
+    for i, lo in enumerate(range(0, rows, chunk)):
+        g = torch.Generator(device=device)
+        g.manual_seed(seed * 1000003 + i)
+        hi = min(rows, lo + chunk)
+        X[lo:hi] = torch.randn((hi - lo, cols), generator=g, device=device, dtype=torch.float32)
+    return X
+
+
+def c3_forest():
+    import tempfile
+    from kfserving_amd.formats import lightgbm_format as lf
+    trees = lf.synthetic_leafwise_trees(1000, 255, 100, seed=1)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, 100, "binary sigmoid:1")
+        return lf.load_lightgbm_model(p), trees, "LightGBM text v3, seeded leaf-wise generator"
+
+
+def c4_forest():
+    """The C4 forest and its raw sklearn tree arrays (for the CPU baseline)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import make_c4_model as mk
+    from kfserving_amd.formats.sklearn_format import (forest_from_sklearn, load_tree_arrays,
+                                                      tree_arrays_from_sklearn)
+    if os.path.exists(mk.MODEL):
+        z = np.load(mk.MODEL, allow_pickle=False)
+        keys = ("children_left", "children_right", "feature", "threshold",
+                "missing_go_to_left", "value")
+        raw = [{k: z[f"t{i}_{k}"] for k in keys} for i in range(int(z["n_trees"]))]
+        return load_tree_arrays(mk.MODEL), raw, ("cached fit on 200k rows "
+                                                 f"({os.path.relpath(mk.MODEL, ROOT)})")
+    rows = 20_000      # the full fit takes minutes: a smaller training set, said so in the output
+    est = mk.fit(rows, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())))
+    raw = [tree_arrays_from_sklearn(e.tree_) for e in est.estimators_]
+    return forest_from_sklearn(est), raw, f"fitted here on {rows} rows (cache absent)"
+
+
+def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_sync,
+               make_engine, cpu_fn=None):
+    """Strong scaling: this rank's block of the batch, K steps, max-over-ranks wall."""
+    import torch
+    from kfserving_amd.forest import OUT_PREDICT, TI_F32
+    lo, hi = strong_shard(total_rows, rank, world)
+    rows = hi - lo
+    eng = make_engine(forest)
+    X = device_normal(rows, n_feat, seed + rank, device)
+    out = torch.empty(rows * forest.output_width(OUT_PREDICT),
+                      dtype=torch.float64 if forest.accum_dtype else torch.float32, device=device)
+    sh = torch.cuda.current_stream().cuda_stream if device != "cpu" else 0
+
+    def step():
+        eng.predict_device(X.data_ptr(), TI_F32, rows, n_feat, n_feat, OUT_PREDICT,
+                           out.data_ptr(), out.numel(), slot=0, stream=sh)
+
+    step()
+    ev = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          if device != "cpu" else None)
+    wall, kms = timed_steps(step, args.config_steps, dev_sync, ev)
+    wall = max_over_ranks(wall, device)
+    res = None
+    if rank == 0:
+        res = {"rows": total_rows, "rows_per_gpu": rows, "scaling": "strong",
+               "steps": args.config_steps, "rows_per_s": total_rows * args.config_steps / wall,
+               "ms_per_step": wall / args.config_steps * 1e3, "kernel_ms_rank0": kms,
+               "layout": LAYOUT_NAMES.get(eng.info()["layout"]),
+               "compulsory_GBps": ((4 * n_feat + out.element_size()) * rows / (kms * 1e-3) / 1e9
+                                   if kms else None)}
+        if cpu_fn is not None and world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_fn(X[:min(rows, 20_000)].cpu().numpy())
+    del X, out
+    eng.close()
+    return res
+
+
+def c3_cpu(trees):
+    def fn(Xs):
+        from oracle import port
+        t0 = time.perf_counter()
+        port.lgb_predict_raw(trees, 1, 100, Xs.astype(np.float64))
+        dt = time.perf_counter() - t0
+        return {"value": Xs.shape[0] / dt, "unit": "rows/s", "cores": port.num_threads(),
+                "kind": "port", "sample": f"{Xs.shape[0]} rows, oracle/c/tree_port.c "
+                                          f"(lightgbm predict loop restated), {dt:.2f} s"}
+    return fn
+
+
+def c4_cpu(raw_trees):
+    def fn(Xs):
+        from oracle import port
+        n = min(Xs.shape[0], 5000)
+        t0 = time.perf_counter()
+        port.sk_predict(raw_trees, 1, 64, Xs[:n])
+        dt = time.perf_counter() - t0
+        return {"value": n / dt, "unit": "rows/s", "cores": port.num_threads(), "kind": "port",
+                "sample": f"{n} rows, oracle/c/tree_port.c (sklearn forest predict "
+                          f"restated), {dt:.2f} s"}
+    return fn
+
+
+# ------------------------------------------------------------------- main
+def run(args, device="cuda", backend="nccl", make_engine=None):
+    """The rank logic of bench.py.  `make_engine(forest)` returns an object with
+    predict_device / predict / info / close (DeviceForest on the GPU; the CPU
+    tests pass a stub).  Returns the JSON line rank 0 prints (None elsewhere)."""
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local_rank)
+    if device == "cuda":
+        torch.cuda.set_device(local_rank)          # before the process group
+        device = f"cuda:{local_rank}"
+        dev_sync = torch.cuda.synchronize
+    else:
+        dev_sync = lambda: None                    # noqa: E731
+    if world > 1 and not dist.is_initialized():
+        kw = {"device_id": torch.device(device)} if backend == "nccl" else {}
+        dist.init_process_group(backend, init_method="env://", **kw)
+    if make_engine is None:
+        from kfserving_amd.engine import DeviceForest
+        make_engine = lambda f: DeviceForest(f, devices=[local_rank])   # noqa: E731
 
-    from kfserving_amd.engine import DeviceForest
     from kfserving_amd.forest import OUT_PREDICT, TI_F32
 
     trees, ti, forest = build_model()
-    dev = DeviceForest(forest, devices=[local_rank])
+    dev = make_engine(forest)
     info = dev.info()
     rows, seed = shard_rows(args.rows, rank, world)
     X_host = np.random.default_rng(seed).standard_normal((rows, N_FEAT), dtype=np.float32)
-    X = torch.from_numpy(X_host).to(f"cuda:{local_rank}")
-    out = torch.empty(rows, dtype=torch.float32, device=f"cuda:{local_rank}")
-    stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
+    X = torch.from_numpy(X_host).to(device)
+    out = torch.empty(rows, dtype=torch.float32, device=device)
+    sh = torch.cuda.current_stream().cuda_stream if device != "cpu" else 0
 
     def step():
         dev.predict_device(X.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
@@ -203,73 +401,65 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    wall = max_over_ranks(wall, f"cuda:{local_rank}")
-    total_rows = rows * world * args.steps
-    value = total_rows / wall
+    ev = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          if device != "cpu" else None)
+    wall, kernel_ms = timed_steps(step, args.steps, dev_sync, ev)
+    if kernel_ms is None:
+        kernel_ms = wall / args.steps * 1e3
+    wall = max_over_ranks(wall, device)
+    value = rows * world * args.steps / wall
 
     nan_variant = None
-    if args.nan_variant > 0 and rank == 0:
+    if args.nan_variant > 0 and rank == 0 and device != "cpu":
         # same shape, seed 1, NaN at random positions: every tile takes the
         # kernel's NaN-checking path (not part of the headline value)
         Xn_host = np.random.default_rng(1).standard_normal((rows, N_FEAT), dtype=np.float32)
         Xn_host[np.random.default_rng(2).random(Xn_host.shape) < args.nan_variant] = np.nan
-        Xn = torch.from_numpy(Xn_host).to(f"cuda:{local_rank}")
-        for _ in range(2):
+        Xn = torch.from_numpy(Xn_host).to(device)
+
+        def nstep():
             dev.predict_device(Xn.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
                                out.data_ptr(), rows, slot=0, stream=sh)
+        nstep()
+        nstep()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
+        e0.record()
         for _ in range(args.steps):
-            dev.predict_device(Xn.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
-                               out.data_ptr(), rows, slot=0, stream=sh)
-        e1.record(stream)
+            nstep()
+        e1.record()
         torch.cuda.synchronize()
         nms = e0.elapsed_time(e1) / args.steps
         nan_variant = {"nan_fraction": args.nan_variant, "kernel_ms": nms,
                        "rows_per_s": rows / (nms * 1e-3)}
         del Xn
 
+    configs = {}
+    for name in [c.strip() for c in args.configs.split(",") if c.strip()]:
+        if name == "c3":
+            f3, t3, src = c3_forest()
+            r = run_config(f3, 100, args.rows3, 3, args, world, rank, device, dev_sync,
+                           make_engine, c3_cpu(t3))
+            if r is not None:
+                r.update(config="C3 LightGBM leaf-wise 1000 trees x 255 leaves, 100 features, "
+                                "float32 input, float64 sigmoid of the raw score", model=src)
+        elif name == "c4":
+            f4, raw4, src = c4_forest()
+            r = run_config(f4, 64, args.rows4, 2, args, world, rank, device, dev_sync,
+                           make_engine, c4_cpu(raw4))
+            if r is not None:
+                r.update(config="C4 sklearn RandomForestRegressor 200 trees max_depth 16, "
+                                "64 features, float32 input, float64 mean", model=src)
+        else:
+            raise ValueError(f"unknown config {name!r}")
+        configs[name] = r
+
+    line = None
     if rank == 0:
-        visits = N_TREES * DEPTH                     # complete trees: every row visits D nodes
-        b_visit = 8 * visits + 4 * N_FEAT + 4        # SURVEY.md 8(d) B_visit
-        achieved = b_visit * rows / (kernel_ms * 1e-3)
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            try:
-                with open(args.traffic_json) as fh:
-                    pmc = json.load(fh)
-                if (pmc.get("rows") == rows and pmc.get("workload") == "c2"
-                        and pmc.get("layout", "heap") == LAYOUT_NAMES.get(info["layout"])):
-                    traffic = pmc.get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
-        roofline = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                    "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
-                    "bytes_per_row_visit_model": b_visit,
-                    "compulsory_GBps": (4 * N_FEAT + 4) * rows / (kernel_ms * 1e-3) / 1e9,
-                    "kernel_ms": kernel_ms}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(trees, ti, X_host, args.cpu_seconds)
         latency = None
-        if args.latency_qps > 0:
+        if args.latency_qps > 0 and device != "cpu":
             latency = batched_latency(dev, N_FEAT, args.latency_qps, args.latency_seconds)
         line = {
             "metric": "predicted rows/sec (500-tree XGB, 28 feat)",
@@ -290,14 +480,23 @@ def main():
                        "rows_per_gpu": rows, "trees": N_TREES, "depth": DEPTH,
                        "features": N_FEAT, "layout": LAYOUT_NAMES.get(info["layout"]),
                        "parallelism": f"rows sharded x{world}"},
-            "roofline": roofline,
+            "roofline": roofline(kernel_ms, rows, LAYOUT_NAMES.get(info["layout"]),
+                                 args.pmc_json),
             "cpu_baseline": cpu,
             "batched_latency": latency,
             "nan_variant": nan_variant,
         }
-        print(json.dumps(line), flush=True)
+        line.update(configs)
+    dev.close()
     if world > 1:
         dist.destroy_process_group()
+    return line
+
+
+def main():
+    line = run(parse_args())
+    if line is not None:
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -524,14 +524,31 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
   const uint32_t tsz = 1u << L;
   const int64_t left_rows = a.n_rows - row0;
   const int rows_here = left_rows < R ? (int)left_rows : R;
+  const bool vec_ok = ((reinterpret_cast<uintptr_t>(X) | (uintptr_t)(a.row_stride * sizeof(XT))) & 15) == 0;
   bool has_nan = false;
   if (tid == 0) *flag = 0;
   for (int f0 = 0; f0 < F; f0 += a.bin_chunk) {
     const int kc = (F - f0) < a.bin_chunk ? (F - f0) : a.bin_chunk;
     __syncthreads();   // temp is free (the previous chunk is searched)
+    constexpr int V = 16 / sizeof(XT);   // elements per 16-byte load
+    const bool vec = vec_ok && (f0 % V) == 0 && (kc % V) == 0 && f0 + kc <= C;
     const uint32_t n = (uint32_t)rows_here * (uint32_t)kc;
     const uint32_t ukc = (uint32_t)kc;
-    for (uint32_t e = tid; e < n; e += R) {
+    if (vec) {
+      // 16 bytes per lane (the row segments are 16-byte aligned): a quarter
+      // (float) or half (double) of the load instructions of the loop below
+      typedef XT xv_t __attribute__((ext_vector_type(V)));
+      const uint32_t kv = ukc / V;
+      const uint32_t nv = (uint32_t)rows_here * kv;
+      for (uint32_t e = tid; e < nv; e += R) {
+        const uint32_t r = e / kv;
+        const uint32_t cv = e - r * kv;
+        const xv_t v = *reinterpret_cast<const xv_t*>(X + (row0 + r) * a.row_stride + f0 + cv * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) temp[(cv * V + j) * R + r] = zero_map(v[j], a.lgb_zero_map);
+      }
+    }
+    for (uint32_t e = vec ? n : tid; e < n; e += R) {
       const uint32_t r = e / ukc;
       const uint32_t c = e - r * ukc;
       const int f = f0 + (int)c;

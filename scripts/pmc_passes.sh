@@ -24,4 +24,9 @@ run pmc_ta 240 --pmc TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum
 run pmc_tcp 240 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum
 run pmc_tlb 240 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum
 run pmc_tcc 240 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum
+if [ -n "$PMC_HBM" ]; then
+  run pmc_fetch 240 --pmc FETCH_SIZE
+  run pmc_write 240 --pmc WRITE_SIZE
+  run pmc_lds 240 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY
+fi
 exit 0
