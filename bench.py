@@ -69,6 +69,8 @@ def parse_args(argv=None):
     p.add_argument("--rows4", type=int, default=10_000_000)
     p.add_argument("--config-steps", type=int, default=2)
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
+    p.add_argument("--host-rows", type=int, default=8_000_000,
+                   help="rows of the host-to-host (PCIe-inclusive) C2 leg (0 = skip)")
     return p.parse_args(argv)
 
 
@@ -255,6 +257,26 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
             "path": "in-process batcher -> ti_predict (host buffers), 1 GPU, no HTTP/JSON"}
 
 
+def host_to_host(dev, X_host, rows, reps=3):
+    """C2 through ti_predict from pageable host memory to host memory (the
+    path the plugins take): chunks of TI_CHUNK_MB (64) MB alternate between two
+    streams, so H2D, kernel and D2H of neighbouring chunks overlap (DESIGN.md
+    5).  PCIe-inclusive; not the headline value."""
+    from kfserving_amd.forest import OUT_PREDICT
+    Xb = np.tile(X_host, (max(1, rows // X_host.shape[0]), 1))
+    dev.predict(Xb[:4096], OUT_PREDICT)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        dev.predict(Xb, OUT_PREDICT)
+        times.append(time.perf_counter() - t0)
+    t = min(times)
+    return {"rows": Xb.shape[0], "chunk_mb": int(os.environ.get("TI_CHUNK_MB", "64")),
+            "rows_per_s": Xb.shape[0] / t, "ms": t * 1e3, "input_GBps": Xb.nbytes / t / 1e9,
+            "reps": reps, "path": "pageable numpy -> pinned chunks -> H2D -> kernel -> D2H -> "
+                                  "numpy, two streams"}
+
+
 # ------------------------------------------------------------ other configs
 def device_normal(rows, cols, seed, device):
     """X ~ N(0,1) float32 generated on the device in 8M-row chunks (seed, chunk)."""
@@ -433,6 +455,10 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
                        "rows_per_s": rows / (nms * 1e-3)}
         del Xn
 
+    host_pipeline = None
+    if args.host_rows > 0 and rank == 0 and device != "cpu":
+        host_pipeline = host_to_host(dev, X_host, args.host_rows)
+
     configs = {}
     for name in [c.strip() for c in args.configs.split(",") if c.strip()]:
         if name == "c3":
@@ -485,6 +511,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             "cpu_baseline": cpu,
             "batched_latency": latency,
             "nan_variant": nan_variant,
+            "host_pipeline": host_pipeline,
         }
         line.update(configs)
     dev.close()

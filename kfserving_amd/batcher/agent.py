@@ -19,7 +19,8 @@ import logging
 import re
 from concurrent.futures import ThreadPoolExecutor
 
-from ..kfserving.kfserver import JSON_CT, _read_request, _serialize, error_response
+from ..kfserving.errors import HTTPError
+from ..kfserving.kfserver import JSON_CT, _BodyTooLarge, _read_request, _serialize, error_response
 from .batcher import MAX_BATCH_SIZE, MAX_LATENCY_MS, Batcher
 
 _PREDICT = re.compile(r":predict$")
@@ -76,6 +77,10 @@ class Agent:
         except (json.JSONDecodeError, UnicodeDecodeError):
             return error_response(400, "can't Unmarshal body")
         instances = req.get("instances") if isinstance(req, dict) else None
+        if instances is not None and not isinstance(instances, list):
+            # a body that does not unmarshal into Request{Instances []interface{}}
+            # (handler.go:234-241)
+            return error_response(400, "can't Unmarshal body")
         if not instances:
             return error_response(400, "no instances in the request")
         # the Go batcher keys one loop per handler; the last request's path wins
@@ -87,11 +92,19 @@ class Agent:
     async def _conn(self, reader, writer):
         try:
             while True:
-                req = await _read_request(reader, 1 << 30)
+                try:
+                    req = await _read_request(reader, 1 << 30)
+                except _BodyTooLarge:
+                    writer.write(_serialize(error_response(413, "Request Entity Too Large"), False))
+                    await writer.drain()
+                    break
                 if req is None:
                     break
                 method, target, version, headers, body = req
-                resp = await self.handle(method, target, headers, body)
+                try:
+                    resp = await self.handle(method, target, headers, body)
+                except HTTPError as e:
+                    resp = error_response(e.status_code, e.reason)
                 keep = headers.get("connection", "").lower() != "close"
                 writer.write(_serialize(resp, keep))
                 await writer.drain()

@@ -143,12 +143,24 @@ def _combine(chunks: List[Any]):
 class ModelBatcher(Batcher):
     """In-process batcher in front of a KFModel's ``predict`` (KFServer
     --max_batchsize): coalesced instances go straight to the model, with no
-    second HTTP hop and no second JSON round trip."""
+    second HTTP hop and no second JSON round trip.
 
-    def __init__(self, model, call, **kw):
+    ``kind="inputs"`` batches lgbserver requests, which the Go batcher rejects
+    with 400 because it only reads ``instances`` (§8(f1) asks
+    for this): each request's ``inputs`` are first turned into the float64
+    matrix its columns select by feature name (``model.batch_inputs``, the
+    same conversion ``predict`` does), the batch is their row concatenation,
+    and ``model.predict_batched`` predicts it."""
+
+    def __init__(self, model, call, kind: str = "instances", **kw):
         self.model = model
+        self.kind = kind
 
-        async def predict_batch(instances):
-            return await call(model.predict, {"instances": instances})
+        if kind == "inputs":
+            async def predict_batch(X):
+                return await call(model.predict_batched, X)
+        else:
+            async def predict_batch(instances):
+                return await call(model.predict, {"instances": instances})
 
         super().__init__(predict_batch, **kw)

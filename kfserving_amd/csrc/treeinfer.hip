@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cmath>
 #include <limits>
@@ -436,6 +437,14 @@ struct DeviceForest {
   size_t hx_cap = 0;
   void* ho_pin = nullptr;
   size_t ho_cap = 0;
+  // the chunk pipeline of batches larger than one chunk (predict_shard): two
+  // lanes, each a stream with its own pinned and device buffers
+  hipStream_t lane_stream[2] = {nullptr, nullptr};
+  void* lane_hx[2] = {nullptr, nullptr};
+  void* lane_ho[2] = {nullptr, nullptr};
+  void* lane_dx[2] = {nullptr, nullptr};
+  void* lane_do[2] = {nullptr, nullptr};
+  size_t lane_x_cap = 0, lane_o_cap = 0;
   int64_t bytes = 0;
   std::mutex mu;
 };
@@ -508,9 +517,22 @@ struct ti_forest {
   int64_t rx_slots = 0;
   int32_t rx_ilp = 8;
   std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
-  // TreeSHAP (TI_OUTPUT_CONTRIB); has_shap = 0 when the forest has no covers
+  // TreeSHAP (TI_OUTPUT_CONTRIB); has_shap = 0 when the forest has no covers.
+  // The path tables are built and uploaded on the first contributions call
+  // (ensure_shap), from a host copy of the arrays they need, so predict-only
+  // serving never pays for them.
   int32_t has_shap = 0, shap_maxl = 0;
   int64_t shap_npaths = 0;
+  std::atomic<bool> shap_ready{false};
+  std::mutex shap_mu;
+  struct ShapSource {
+    ti_forest_desc desc;
+    std::vector<int64_t> tree_offset;
+    std::vector<int32_t> tree_group, feature, left, right;
+    std::vector<double> threshold, leaf_value, base_margin, cover;
+    std::vector<uint8_t> flags;
+  };
+  std::unique_ptr<ShapSource> shap_src;
   std::vector<ShapPath> h_paths;
   std::vector<ShapElem> h_elems;
   std::vector<double> h_path_leaf, h_shap_bias;
@@ -557,6 +579,16 @@ void free_device(DeviceForest& d) {
   if (d.ho_pin) (void)hipHostFree(d.ho_pin);
   d.hx_pin = d.ho_pin = nullptr;
   d.hx_cap = d.ho_cap = 0;
+  for (int l = 0; l < 2; ++l) {
+    if (d.lane_hx[l]) (void)hipHostFree(d.lane_hx[l]);
+    if (d.lane_ho[l]) (void)hipHostFree(d.lane_ho[l]);
+    if (d.lane_dx[l]) (void)hipFree(d.lane_dx[l]);
+    if (d.lane_do[l]) (void)hipFree(d.lane_do[l]);
+    if (d.lane_stream[l]) (void)hipStreamDestroy(d.lane_stream[l]);
+    d.lane_hx[l] = d.lane_ho[l] = d.lane_dx[l] = d.lane_do[l] = nullptr;
+    d.lane_stream[l] = nullptr;
+  }
+  d.lane_x_cap = d.lane_o_cap = 0;
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d.heap32 = d.heap64 = nullptr;
   d.heap_leaf_ids = d.root = d.exp_leaf_ids = d.tree_group = nullptr;
@@ -1324,10 +1356,44 @@ struct ShapBuilder {
   }
 };
 
-void build_shap(const ti_forest_desc* d, ti_forest* f) {
+// At create: whether contributions are possible (covers, no categorical
+// splits), and the host copy build_shap will read on first use.
+void keep_shap_source(const ti_forest_desc* d, ti_forest* f) {
   if (!d->cover) return;
   for (int64_t g = 0; g < d->n_nodes; ++g)
     if (d->feature[g] >= 0 && (d->flags[g] & TI_NODE_CATEGORICAL)) return;
+  auto src = std::make_unique<ti_forest::ShapSource>();
+  const int64_t N = d->n_nodes, T = d->n_trees;
+  src->tree_offset.assign(d->tree_offset, d->tree_offset + T + 1);
+  if (d->tree_group) src->tree_group.assign(d->tree_group, d->tree_group + T);
+  src->feature.assign(d->feature, d->feature + N);
+  src->left.assign(d->left, d->left + N);
+  src->right.assign(d->right, d->right + N);
+  src->threshold.assign(d->threshold, d->threshold + N);
+  src->leaf_value.assign(d->leaf_value, d->leaf_value + N * d->leaf_width);
+  src->base_margin.assign(d->base_margin, d->base_margin + d->n_groups);
+  src->cover.assign(d->cover, d->cover + N);
+  src->flags.assign(d->flags, d->flags + N);
+  src->desc = *d;
+  src->desc.tree_offset = src->tree_offset.data();
+  src->desc.tree_group = src->tree_group.empty() ? nullptr : src->tree_group.data();
+  src->desc.feature = src->feature.data();
+  src->desc.left = src->left.data();
+  src->desc.right = src->right.data();
+  src->desc.threshold = src->threshold.data();
+  src->desc.leaf_value = src->leaf_value.data();
+  src->desc.base_margin = src->base_margin.data();
+  src->desc.cover = src->cover.data();
+  src->desc.flags = src->flags.data();
+  src->desc.leaf_id = nullptr;
+  src->desc.cat_bits = nullptr;
+  src->desc.cat_offset = nullptr;
+  src->desc.cat_nwords = nullptr;
+  f->shap_src = std::move(src);
+  f->has_shap = 1;
+}
+
+void build_shap(const ti_forest_desc* d, ti_forest* f) {
   const int K = d->n_groups;
   std::vector<double> bias(K);
   for (int k = 0; k < K; ++k) bias[k] = d->base_margin[k] * d->average_divisor;
@@ -1344,7 +1410,6 @@ void build_shap(const ti_forest_desc* d, ti_forest* f) {
   f->h_shap_bias.resize(K);
   for (int k = 0; k < K; ++k) f->h_shap_bias[k] = bias[k] / d->average_divisor;
   f->shap_npaths = static_cast<int64_t>(f->h_paths.size());
-  f->has_shap = 1;
 }
 
 int upload_device(ti_forest* f, DeviceForest& d, int device) {
@@ -1353,12 +1418,6 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
   TI_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   int rc;
   if ((rc = upload(&d.tree_group, f->h_group, &d.bytes))) return rc;
-  if (f->has_shap) {
-    if ((rc = upload(&d.shap_paths, f->h_paths, &d.bytes))) return rc;
-    if ((rc = upload(&d.shap_elems, f->h_elems, &d.bytes))) return rc;
-    if ((rc = upload(&d.shap_leaf, f->h_path_leaf, &d.bytes))) return rc;
-    if ((rc = upload(&d.shap_bias, f->h_shap_bias, &d.bytes))) return rc;
-  }
   if (f->layout == 0) {
     if ((rc = upload(&d.heap32, f->h_heap32, &d.bytes))) return rc;
     if ((rc = upload(&d.heap64, f->h_heap64, &d.bytes))) return rc;
@@ -1764,10 +1823,113 @@ int grow(void** buf, size_t* cap, size_t need, bool pinned = false) {
 int launch_any(ti_forest* f, int slot, const void* X, int xdt, int64_t rows, int32_t cols,
                int64_t stride, int kind, void* out, hipStream_t stream);
 
+// Host copies into / out of pinned staging: large copies split over threads
+// (one thread moves ~10 GB/s from pageable memory; PCIe Gen5 x16 takes ~55).
+void copy_parallel(void* dst, const void* src, size_t n) {
+  constexpr size_t kPerThread = 8u << 20;
+  const size_t want = std::min<size_t>(8, n / kPerThread);
+  if (want < 2) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t part = (n / want + 63) & ~size_t(63);
+  for (size_t i = 0; i < want; ++i) {
+    const size_t lo = i * part;
+    if (lo >= n) break;
+    const size_t len = std::min(part, n - lo);
+    th.emplace_back([=]() {
+      std::memcpy(static_cast<unsigned char*>(dst) + lo, static_cast<const unsigned char*>(src) + lo, len);
+    });
+  }
+  for (auto& t : th) t.join();
+}
+
+// Rows per chunk of the host pipeline: TI_CHUNK_MB (default 64) of input,
+// a multiple of 512 rows (whole tiles).
+int64_t chunk_rows(size_t row_bytes) {
+  const int mb = env_int("TI_CHUNK_MB", 64);
+  int64_t r = static_cast<int64_t>((static_cast<size_t>(std::max(mb, 1)) << 20) / std::max<size_t>(row_bytes, 1));
+  r = std::max<int64_t>(512, r & ~int64_t(511));
+  return r;
+}
+
+// Batches larger than one chunk: chunks alternate between two lanes (streams
+// with their own pinned and device buffers).  While lane A runs chunk c
+// (H2D -> kernel -> D2H), the host copies chunk c+1 into lane B's pinned
+// buffer and enqueues it, so B's H2D overlaps A's kernel; before lane A takes
+// chunk c+2 the host waits for chunk c and copies its result out.  Pinned
+// memory is 2 x (chunk in + chunk out) whatever the batch size.
+int predict_pipelined(ti_forest* f, int slot, DeviceForest& d, const unsigned char* X, int xdt,
+                      int64_t rows, int32_t cols, int64_t stride, int kind, unsigned char* out,
+                      int64_t ch) {
+  const size_t xs = dtype_size(xdt);
+  const size_t os = dtype_size(output_dtype(f, kind)) * output_width(f, kind);
+  const size_t x_row = static_cast<size_t>(stride) * xs;
+  const size_t x_cap = static_cast<size_t>(ch) * x_row;
+  const size_t o_cap = static_cast<size_t>(ch) * os;
+  if (d.lane_x_cap < x_cap || d.lane_o_cap < o_cap) {
+    for (int l = 0; l < 2; ++l) {
+      if (d.lane_hx[l]) (void)hipHostFree(d.lane_hx[l]);
+      if (d.lane_ho[l]) (void)hipHostFree(d.lane_ho[l]);
+      if (d.lane_dx[l]) (void)hipFree(d.lane_dx[l]);
+      if (d.lane_do[l]) (void)hipFree(d.lane_do[l]);
+      d.lane_hx[l] = d.lane_ho[l] = d.lane_dx[l] = d.lane_do[l] = nullptr;
+    }
+    d.lane_x_cap = d.lane_o_cap = 0;
+    for (int l = 0; l < 2; ++l) {
+      TI_HIP(hipHostMalloc(&d.lane_hx[l], x_cap, hipHostMallocDefault));
+      TI_HIP(hipHostMalloc(&d.lane_ho[l], o_cap, hipHostMallocDefault));
+      TI_HIP(hipMalloc(&d.lane_dx[l], x_cap));
+      TI_HIP(hipMalloc(&d.lane_do[l], o_cap));
+    }
+    d.lane_x_cap = x_cap;
+    d.lane_o_cap = o_cap;
+  }
+  for (int l = 0; l < 2; ++l)
+    if (!d.lane_stream[l]) TI_HIP(hipStreamCreateWithFlags(&d.lane_stream[l], hipStreamNonBlocking));
+  const int64_t n_chunks = (rows + ch - 1) / ch;
+  int64_t pending[2] = {-1, -1};   // chunk whose result lane l still holds
+  auto drain = [&](int l) -> int {
+    if (pending[l] < 0) return TI_OK;
+    TI_HIP(hipStreamSynchronize(d.lane_stream[l]));
+    const int64_t c = pending[l];
+    const int64_t n = std::min(ch, rows - c * ch);
+    copy_parallel(out + static_cast<size_t>(c * ch) * os, d.lane_ho[l], static_cast<size_t>(n) * os);
+    pending[l] = -1;
+    return TI_OK;
+  };
+  int rc = TI_OK;
+  for (int64_t c = 0; c < n_chunks && rc == TI_OK; ++c) {
+    const int l = static_cast<int>(c & 1);
+    if ((rc = drain(l))) break;
+    const int64_t r0 = c * ch;
+    const int64_t n = std::min(ch, rows - r0);
+    const size_t xb = static_cast<size_t>((n - 1) * stride + cols) * xs;
+    copy_parallel(d.lane_hx[l], X + static_cast<size_t>(r0) * x_row, xb);
+    hipStream_t st = d.lane_stream[l];
+    TI_HIP(hipMemcpyAsync(d.lane_dx[l], d.lane_hx[l], xb, hipMemcpyHostToDevice, st));
+    if ((rc = launch_any(f, slot, d.lane_dx[l], xdt, n, cols, stride, kind, d.lane_do[l], st)))
+      break;
+    TI_HIP(hipMemcpyAsync(d.lane_ho[l], d.lane_do[l], static_cast<size_t>(n) * os,
+                          hipMemcpyDeviceToHost, st));
+    pending[l] = c;
+  }
+  // the other lane first: it holds the older chunk
+  const int last = static_cast<int>((n_chunks - 1) & 1);
+  const int r1 = drain(last ^ 1);
+  const int r2 = drain(last);
+  return rc ? rc : (r1 ? r1 : r2);
+}
+
 int predict_shard(ti_forest* f, int slot, DeviceForest& d, const unsigned char* X, int xdt,
                   int64_t rows, int32_t cols, int64_t stride, int kind, unsigned char* out) {
   std::lock_guard<std::mutex> lk(d.mu);
   TI_HIP(hipSetDevice(d.device));
+  {
+    const int64_t ch = chunk_rows(static_cast<size_t>(stride) * dtype_size(xdt));
+    if (rows > ch) return predict_pipelined(f, slot, d, X, xdt, rows, cols, stride, kind, out, ch);
+  }
   const size_t xs = dtype_size(xdt);
   const size_t x_elems = static_cast<size_t>((rows - 1) * stride + cols);
   const size_t out_bytes = static_cast<size_t>(rows * output_width(f, kind)) *
@@ -1780,13 +1942,13 @@ int predict_shard(ti_forest* f, int slot, DeviceForest& d, const unsigned char* 
   if ((rc = grow(&d.ho_pin, &d.ho_cap, out_bytes, true))) return rc;
   // caller memory -> pinned staging -> DMA; keeps H2D/D2H asynchronous and at
   // PCIe rate whatever kind of host memory the caller holds
-  std::memcpy(d.hx_pin, X, x_bytes);
+  copy_parallel(d.hx_pin, X, x_bytes);
   TI_HIP(hipMemcpyAsync(d.x_buf, d.hx_pin, x_bytes, hipMemcpyHostToDevice, d.stream));
   if ((rc = launch_any(f, slot, d.x_buf, xdt, rows, cols, stride, kind, d.out_buf, d.stream)))
     return rc;
   TI_HIP(hipMemcpyAsync(d.ho_pin, d.out_buf, out_bytes, hipMemcpyDeviceToHost, d.stream));
   TI_HIP(hipStreamSynchronize(d.stream));
-  std::memcpy(out, d.ho_pin, out_bytes);
+  copy_parallel(out, d.ho_pin, out_bytes);
   return TI_OK;
 }
 
@@ -1923,11 +2085,45 @@ int launch_chunked(ti_forest* f, int slot, const void* X, int xdt, int64_t rows,
 // unique features: path slices over blockIdx.y, partials summed in slice
 // order by contrib_slices_kernel.  Otherwise contrib_kernel, whose float32
 // forests accumulate in a float64 scratch.
+// First contributions call: build the path tables on the host and upload them
+// to every device replica (under the forest's lock; later calls see
+// shap_ready and skip it).
+int ensure_shap(ti_forest* f) {
+  if (f->shap_ready.load(std::memory_order_acquire)) return TI_OK;
+  std::lock_guard<std::mutex> lk(f->shap_mu);
+  if (f->shap_ready.load(std::memory_order_relaxed)) return TI_OK;
+  build_shap(&f->shap_src->desc, f);
+  int dev0 = 0;
+  TI_HIP(hipGetDevice(&dev0));
+  int rc = TI_OK;
+  for (auto& dp : f->devs) {
+    DeviceForest& d = *dp;
+    TI_HIP(hipSetDevice(d.device));
+    if ((rc = upload(&d.shap_paths, f->h_paths, &d.bytes)) ||
+        (rc = upload(&d.shap_elems, f->h_elems, &d.bytes)) ||
+        (rc = upload(&d.shap_leaf, f->h_path_leaf, &d.bytes)) ||
+        (rc = upload(&d.shap_bias, f->h_shap_bias, &d.bytes)))
+      break;
+  }
+  TI_HIP(hipSetDevice(dev0));
+  if (rc) return rc;
+  f->h_paths.clear(); f->h_paths.shrink_to_fit();
+  f->h_elems.clear(); f->h_elems.shrink_to_fit();
+  f->h_path_leaf.clear(); f->h_path_leaf.shrink_to_fit();
+  f->shap_src.reset();
+  f->shap_ready.store(true, std::memory_order_release);
+  return TI_OK;
+}
+
 int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows,
                    int32_t cols, int64_t stride, void* out, hipStream_t stream) {
   if (!f->has_shap)
     return fail(TI_ERR_UNSUPPORTED,
                 "contributions need node covers (ti_forest_desc.cover) and no categorical splits");
+  {
+    const int rc = ensure_shap(f);
+    if (rc) return rc;
+  }
   const int64_t W = static_cast<int64_t>(f->K) * (f->F + 1);
   const int64_t n_paths = static_cast<int64_t>(d.shap_paths ? 1 : 0) * f->shap_npaths;
   static const int force_generic = env_int("TI_SHAP_GENERIC", 0);
@@ -2336,7 +2532,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
       }
     }
   }
-  build_shap(desc, f.get());
+  keep_shap_source(desc, f.get());
   for (int i = 0; i < n_devices; ++i) {
     f->devs.emplace_back(new DeviceForest());
     rc = upload_device(f.get(), *f->devs.back(), devices[i]);
@@ -2378,12 +2574,6 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   }
   f->h_rx_base.clear(); f->h_rx_base.shrink_to_fit();
   f->h_rx_nint.clear(); f->h_rx_nint.shrink_to_fit();
-  f->h_paths.clear();
-  f->h_paths.shrink_to_fit();
-  f->h_elems.clear();
-  f->h_elems.shrink_to_fit();
-  f->h_path_leaf.clear();
-  f->h_path_leaf.shrink_to_fit();
   for (auto& bi : f->bh) {
     bi.img.clear();
     bi.img.shrink_to_fit();

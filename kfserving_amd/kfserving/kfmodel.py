@@ -2,8 +2,8 @@
 
 Same constructor, attributes (name, ready, protocol, predictor_host,
 explainer_host, timeout), and load / preprocess / postprocess / predict /
-explain contract.  preprocess unwraps a structured CloudEvent dict exactly as
-kfmodel.py:75-81 does; predict/explain forward to ``predictor_host`` over HTTP
+explain contract.  preprocess unwraps a binary-mode CloudEvent (kfmodel.py:58-70)
+and a structured CloudEvent dict (kfmodel.py:75-81) as the reference does; predict/explain forward to ``predictor_host`` over HTTP
 when set (kfmodel.py:88-122), otherwise raise NotImplementedError.
 """
 from __future__ import annotations
@@ -14,6 +14,7 @@ import urllib.error
 import urllib.request
 from typing import Dict
 
+from .cloudevent import CloudEvent
 from .errors import HTTPError
 
 PREDICTOR_URL_FORMAT = "http://{0}/v1/models/{1}:predict"
@@ -39,6 +40,19 @@ class KFModel:
         return self.ready
 
     def preprocess(self, request: Dict) -> Dict:
+        # binary-mode CloudEvent (kfmodel.py:58-70): its data, JSON-decoded when
+        # it is bytes; undecodable bytes are passed on, unless the event says
+        # its content is JSON (400)
+        if isinstance(request, CloudEvent):
+            response = request.data
+            if isinstance(response, bytes):
+                try:
+                    response = json.loads(response.decode("UTF-8"))
+                except (json.JSONDecodeError, UnicodeDecodeError) as e:
+                    if request._attributes.get("content-type") in (
+                            "application/cloudevents+json", "application/json"):
+                        raise HTTPError(400, "Unrecognized request format: %s" % e)
+            return response
         # structured CloudEvent: {"time","type","source","id","specversion","data"}
         if isinstance(request, dict) and all(k in request for k in _CE_STRUCTURED_KEYS):
             return request["data"]

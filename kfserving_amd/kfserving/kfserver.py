@@ -35,7 +35,7 @@ from concurrent.futures import ThreadPoolExecutor
 from http import HTTPStatus
 from typing import Dict, List, Optional, Tuple
 
-from . import fastjson
+from . import cloudevent, fastjson
 from .errors import HTTPError
 from .kfmodel import KFModel
 from .kfmodel_repository import KFModelRepository
@@ -121,9 +121,17 @@ def pin_worker_device(index: int, workers: int) -> None:
         os.environ["TREEINFER_DEVICES"] = str(index % n)
 
 
+def status_reason(reason: str) -> str:
+    """The reason phrase as it may stand in a status line: CR / LF (which
+    would split the response) become spaces; characters outside latin-1 are
+    replaced when the line is encoded (_serialize).  The full text stays in the
+    error page body (UTF-8)."""
+    return reason.replace("\r", " ").replace("\n", " ")
+
+
 def error_response(code: int, reason: str) -> Response:
     page = "<html><title>%d: %s</title><body>%d: %s</body></html>" % (code, reason, code, reason)
-    return code, reason, {"Content-Type": HTML_CT}, page.encode("utf-8")
+    return code, status_reason(reason), {"Content-Type": HTML_CT}, page.encode("utf-8")
 
 
 class Application:
@@ -217,6 +225,8 @@ class Application:
         return await asyncio.get_running_loop().run_in_executor(self.executor, fn, request)
 
     async def predict(self, headers, body, name):
+        if cloudevent.has_binary_headers(headers):
+            return await self._predict_binary_ce(headers, body, name)
         X = fastjson.parse_instances(body) if self.fast_json else None
         if X is None:
             try:
@@ -234,17 +244,46 @@ class Application:
                 request = json.loads(body)
         request = model.preprocess(request)
         request = self.validate(request)
-        if self._batcher_factory is not None and isinstance(request, dict) \
-                and "instances" in request:
-            batcher = self._batchers.get(name)
-            if batcher is None or batcher.model is not model:
-                batcher = self._batcher_factory(model, self._call)
-                self._batchers[name] = batcher
-            response = await batcher.submit(request["instances"])
-            return _ok(model.postprocess(response))
+        return _ok(await self._predict_request(model, name, request))
+
+    async def _predict_request(self, model, name, request):
+        """predict -> postprocess, through the batcher when one is configured:
+        ``instances`` as they are, lgbserver ``inputs`` as the float64 matrix
+        their columns select (``batch_inputs``), one batcher per model and
+        request kind."""
+        if self._batcher_factory is not None and isinstance(request, dict):
+            chunk, kind = None, None
+            if "instances" in request:
+                chunk, kind = request["instances"], "instances"
+            elif "inputs" in request and hasattr(model, "batch_inputs"):
+                try:
+                    chunk, kind = model.batch_inputs(request), "inputs"
+                except Exception as e:
+                    raise HTTPError(500, "Failed to predict %s" % e)
+            if kind is not None:
+                key = (name, kind)
+                batcher = self._batchers.get(key)
+                if batcher is None or batcher.model is not model:
+                    batcher = self._batcher_factory(model, self._call, kind)
+                    self._batchers[key] = batcher
+                response = await batcher.submit(chunk)
+                return model.postprocess(response)
         response = await self._call(model.predict, request)
-        response = model.postprocess(response)
-        return _ok(response)
+        return model.postprocess(response)
+
+    async def _predict_binary_ce(self, headers, body, name):
+        """Binary-mode CloudEvent in, binary-mode CloudEvent out
+        (handlers/http.py:55-66, 81-91)."""
+        try:
+            event = cloudevent.from_binary_http(headers, body)
+        except cloudevent.CloudEventError as e:
+            raise HTTPError(HTTPStatus.BAD_REQUEST, "Cloud Event Exceptions: %s" % e)
+        model = self.get_model(name)
+        request = self.validate(model.preprocess(event))
+        response = await self._predict_request(model, name, request)
+        hdrs, payload = cloudevent.to_binary_http(event, response)
+        hdrs.setdefault("Content-Type", HTML_CT)    # tornado's default for written bytes
+        return 200, "OK", hdrs, payload
 
     async def explain(self, headers, body, name):
         model = self.get_model(name)
@@ -323,16 +362,16 @@ async def _read_request(reader: asyncio.StreamReader, max_body: int):
 
 def _serialize(resp: Response, keep_alive: bool) -> bytes:
     code, reason, hdrs, body = resp
-    out = [f"HTTP/1.1 {code} {reason}\r\n"]
+    out = [f"HTTP/1.1 {code} {status_reason(reason)}\r\n"]
     hdrs = dict(hdrs)
     hdrs["Content-Length"] = str(len(body))
     hdrs.setdefault("Server", "kfserving-amd")
     if not keep_alive:
         hdrs["Connection"] = "close"
     for k, v in hdrs.items():
-        out.append(f"{k}: {v}\r\n")
+        out.append(f"{k}: {status_reason(str(v))}\r\n")
     out.append("\r\n")
-    return "".join(out).encode("latin-1") + body
+    return "".join(out).encode("latin-1", errors="replace") + body
 
 
 class KFServer:
@@ -362,8 +401,9 @@ class KFServer:
             from ..batcher.batcher import ModelBatcher
             size, lat = self.max_batchsize, self.max_latency_ms
 
-            def factory(model, call):
-                return ModelBatcher(model, call, max_batch_size=size, max_latency_ms=lat)
+            def factory(model, call, kind="instances"):
+                return ModelBatcher(model, call, kind=kind, max_batch_size=size,
+                                    max_latency_ms=lat)
         return Application(self.registered_models, batcher_factory=factory,
                            fast_json=self.fast_json)
 

@@ -48,3 +48,18 @@ class LightGBMModel(GPUForestMixin, KFModel):
             return {"predictions": result.tolist()}
         except Exception as e:
             raise Exception("Failed to predict %s" % e)
+
+    # KFServer's in-process batcher (kfserving_amd.batcher.ModelBatcher, kind
+    # "inputs"): one request's rows as the float64 matrix its columns select,
+    # then one predict over the concatenated rows of a batch
+    def batch_inputs(self, request: Dict) -> np.ndarray:
+        X = self.request_matrix(request)
+        if X.shape[0] == 0:
+            raise ValueError("no rows in the request")
+        return X
+
+    def predict_batched(self, X: np.ndarray) -> Dict:
+        try:
+            return {"predictions": self.predict_matrix(X).tolist()}
+        except Exception as e:
+            raise Exception("Failed to predict %s" % e)

@@ -64,7 +64,11 @@ class SKLearnModel(GPUForestMixin, KFModel):  # pylint:disable=c-extension-no-me
                              % (X.shape[1], f.objective, f.n_features))
         if not f.meta.get("allow_nan", True) and np.isnan(X).any():
             raise ValueError("Input X contains NaN.")   # GradientBoosting: validate_data
-        if np.isinf(X).any():
+        # sklearn converts to float32 (DTYPE) before its finiteness check, so a
+        # finite float64 beyond the float32 range is rejected like infinity
+        with np.errstate(over="ignore"):
+            X32 = X.astype(np.float32)
+        if np.isinf(X32).any():
             raise ValueError("Input X contains infinity or a value too large for "
                              "dtype('float32').")
         return X

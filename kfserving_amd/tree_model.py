@@ -89,14 +89,30 @@ def xgb_matrix_from_list(instances) -> np.ndarray:
     return X32
 
 
+def _numeric_column(values) -> bool:
+    seen_number = False
+    for v in values:
+        if v is None:
+            continue
+        if not isinstance(v, (bool, int, float)):
+            return False
+        seen_number = True
+    return seen_number or len(values) == 0
+
+
 def lgb_matrix_from_inputs(inputs: List[dict], feature_names: List[str]) -> np.ndarray:
     """``pd.concat([pd.DataFrame(i, columns=booster.feature_name()) ...])`` then
     lightgbm's float conversion (lgbserver/model.py:46-51): columns chosen by
     name, absent columns NaN, extra keys dropped, float64."""
     fast = []
     for inp in inputs:
-        if not isinstance(inp, dict) or not all(isinstance(v, (list, tuple))
-                                                for v in inp.values()):
+        # the fast path takes only what pandas would type as numbers: lists of
+        # bool / int / float (None allowed beside numbers, where pandas infers
+        # float); anything else (numeric strings, all-None columns, objects)
+        # goes through pandas, which applies lightgbm's dtype check
+        if not isinstance(inp, dict) or not all(
+                isinstance(v, (list, tuple)) and _numeric_column(v) for k, v in inp.items()
+                if k in feature_names):
             fast = None
             break
         n = {len(inp[k]) for k in feature_names if k in inp}

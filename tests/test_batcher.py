@@ -150,7 +150,18 @@ def test_agent_proxy_end_to_end():
     assert sorted(b["predictions"][0][0] for _, b in out) == [0, 2, 4, 6]
     c = http.client.HTTPConnection("127.0.0.1", a.port, timeout=30)
     c.request("GET", "/v1/models/m")
-    assert c.getresponse().status == 200                 # non-predict paths proxied
+    r = c.getresponse()
+    r.read()
+    assert r.status == 200                               # non-predict paths proxied
+    # instances that do not unmarshal into []interface{}: 400 (handler.go:234-241),
+    # and the connection stays usable
+    for bad in (b'{"instances": {"a": 1}}', b'{"instances": "x"}', b'{"instances": 3}'):
+        c.request("POST", "/v1/models/m:predict", body=bad)
+        r = c.getresponse()
+        assert r.status == 400 and b"can't Unmarshal body" in r.read()
+    c.request("POST", "/v1/models/m:predict", body=b'{"instances": []}')
+    r = c.getresponse()
+    assert r.status == 400 and b"no instances in the request" in r.read()
     backend.stop()
 
 

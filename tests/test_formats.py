@@ -247,3 +247,28 @@ def test_sklearn_gradient_boosting_restated_bit_exact():
         assert np.array_equal(raw.reshape(want.shape), want)
         lab = f.meta["classes"].take(canon_eval.predict(f, Xt, OUT_PREDICT).astype(np.int64))
         assert np.array_equal(lab, est.predict(Xt))
+
+
+def test_sklearn_request_checks_in_float32(golden, tmp_path):
+    """sklearn converts X to float32 before its finiteness check, so a finite
+    float64 beyond the float32 range is rejected like infinity."""
+    import shutil
+    from kfserving_amd.sklearnserver import SKLearnModel
+    shutil.copy(os.path.join(golden, "sk_rf_reg_model.npz"), str(tmp_path / "model.npz"))
+    model = SKLearnModel("sk", str(tmp_path))
+    assert model.load()
+    row = [0.5] * model._forest.n_features
+    model.request_matrix({"instances": [row]})
+    for v in (1e39, -1e39, float("inf")):
+        with pytest.raises(ValueError, match="infinity or a value too large"):
+            model.request_matrix({"instances": [[v] + row[1:]]})
+
+
+def test_lgb_inputs_dtype_rules():
+    """Columns pandas would not type as numbers fail lightgbm's dtype check
+    (numeric strings, all-None columns); None beside numbers reads NaN."""
+    X = lgb_matrix_from_inputs([{"a": [1, 2.5], "b": [None, 3]}], ["a", "b"])
+    assert np.isnan(X[0, 1]) and X[1, 1] == 3
+    for bad in ([{"a": ["1.5"], "b": [1]}], [{"a": [None], "b": [1]}]):
+        with pytest.raises(ValueError, match="dtypes"):
+            lgb_matrix_from_inputs(bad, ["a", "b"])

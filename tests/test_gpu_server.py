@@ -68,3 +68,22 @@ def test_sklearnserver_http_and_batcher(golden, tmp_path):
     assert code == 200 and res["message"] == "" and res["batchId"]
     assert np.array_equal(np.array(res["predictions"]), want)
     s.stop()
+
+
+def test_lgbserver_inputs_batched_gpu(golden, tmp_path):
+    """Concurrent lgbserver ``inputs`` requests share a batch (one batchId per
+    batch) and each gets lgb_ref.predict on its own rows."""
+    from oracle import lgb_ref
+    from tests.test_lgb_batching import _lgb_model, run_batched
+    model = _lgb_model(golden, tmp_path, stub=False)
+    reqs, results = run_batched(model)
+    m = lgb_ref.read_lgb_text(os.path.join(golden, "lgb_iris_v3.txt"))
+    bodies = [json.loads(b) for _, _, b in results]
+    assert all(c == 200 for c, _, _ in results)
+    assert len({b["batchId"] for b in bodies}) < len(bodies)
+    for req, b in zip(reqs, bodies):
+        X = model.request_matrix(req)
+        np.testing.assert_allclose(np.array(b["predictions"]), lgb_ref.predict(m, X),
+                                   rtol=1e-5, atol=0)
+        assert np.array_equal(np.argmax(b["predictions"], axis=1),
+                              np.argmax(lgb_ref.predict(m, X), axis=1))

@@ -277,3 +277,128 @@ def test_fast_json_not_for_custom_preprocess_or_plain_models(serve):
     assert code == 200 and m1.seen == ["list"]
     code, _, body = s.fetch("/v1/models/s:predict", "POST", b'{"instances": [[1, 2]]}')
     assert code == 200 and json.loads(body) == {"predictions": [[2, 4]]}
+
+
+# ------------------------------------------------ binary-mode CloudEvents
+# The request a cloudevents ``to_binary(dummy_cloud_event(data, set_contenttype=True))``
+# makes (python/kfserving/test/test_server.py:35-48), sent as tornado's test
+# client sends it (POST bodies default to application/x-www-form-urlencoded).
+CE_HEADERS = {
+    "ce-specversion": "1.0",
+    "ce-id": "36077800-0c23-4f38-a0b4-01f4369f670a",
+    "ce-source": "https://example.com/event-producer",
+    "ce-type": "com.example.sampletype1",
+    "ce-time": "2021-01-28T21:04:43.144141+00:00",
+    "ce-content-type": "application/json",
+    "Content-Type": "application/x-www-form-urlencoded",
+}
+
+
+class RawBytesModel(KFModel):
+    """Like the reference's DummyAvroCEModel: its own preprocess keeps the
+    binary event's attributes and raw bytes (here: echoes their length)."""
+
+    def __init__(self, name):
+        super().__init__(name)
+        self.ready = True
+
+    def preprocess(self, request):
+        from kfserving_amd.kfserving.cloudevent import CloudEvent
+        assert isinstance(request, CloudEvent)
+        a = request._attributes
+        assert a["specversion"] == "1.0" and a["source"] == "https://example.com/event-producer"
+        assert a["type"] == "com.example.sampletype1"
+        assert a["datacontenttype"] == "application/x-www-form-urlencoded"
+        assert a["content-type"] == "application/json"
+        return request.data
+
+    async def predict(self, request):
+        return {"predictions": [[len(request), request[:1].decode("latin-1")]]}
+
+
+def _check_ce_response(code, hdrs, body, want_body):
+    assert code == 200
+    assert body == want_body
+    h = {k.lower(): v for k, v in hdrs.items()}
+    assert h["content-type"] == "application/x-www-form-urlencoded"
+    assert h["ce-specversion"] == "1.0"
+    assert h["ce-id"] == "36077800-0c23-4f38-a0b4-01f4369f670a"
+    assert h["ce-source"] == "https://example.com/event-producer"
+    assert h["ce-type"] == "com.example.sampletype1"
+    assert h["ce-datacontenttype"] == "application/x-www-form-urlencoded"
+    assert h["ce-time"] > "2021-01-28T21:04:43.144141+00:00"
+
+
+@pytest.mark.parametrize("batch", [0, 4])
+def test_cloudevent_binary(serve, batch):
+    """test_server.py:262-297 (binary dict / bytes data) and :299-303 (bad JSON,
+    bad UTF-8: 400 with the decoder's message)."""
+    server = KFServer(registered_models=KFModelRepository(), max_batchsize=batch,
+                      max_latency_ms=5)
+    m = DummyModel("TestModel")
+    m.load()
+    server.register_model(m)
+    s = serve(server)
+    for body in (json.dumps({"instances": [[1, 2]]}).encode(), b'{"instances":[[1,2]]}'):
+        code, hdrs, out = s.fetch("/v1/models/TestModel:predict", "POST", body, CE_HEADERS)
+        if batch:
+            out = json.loads(out)
+            assert out["predictions"] == [[1, 2]] and out["batchId"]
+            out = b'{"predictions": [[1, 2]]}'
+        _check_ce_response(code, hdrs, out, b'{"predictions": [[1, 2]]}')
+    code, _, out = s.fetch("/v1/models/TestModel:predict", "POST", b"{", CE_HEADERS)
+    assert code == 400
+    assert b"Unrecognized request format: Expecting property name enclosed in double quotes" in out
+    code, _, out = s.fetch("/v1/models/TestModel:predict", "POST", b"0\x80\x80\x06World!\x00\x00",
+                           CE_HEADERS)
+    assert code == 400
+    assert (b"Unrecognized request format: 'utf-8' codec can't decode byte 0x80 in position 1: "
+            b"invalid start byte") in out
+    # missing a required attribute: not a binary event at all -> JSON path
+    hdrs = {k: v for k, v in CE_HEADERS.items() if k != "ce-id"}
+    code, _, out = s.fetch("/v1/models/TestModel:predict", "POST", b'{"instances":[[3]]}', hdrs)
+    assert code == 200 and json.loads(out)["predictions"] == [[3]]
+    # a bad specversion
+    hdrs = dict(CE_HEADERS, **{"ce-specversion": "9.9"})
+    code, _, out = s.fetch("/v1/models/TestModel:predict", "POST", b'{"instances":[[3]]}', hdrs)
+    assert code == 400 and b"Cloud Event Exceptions" in out
+
+
+def test_cloudevent_binary_raw_bytes(serve):
+    """test_server.py:314-341 with the Avro payload replaced by raw bytes the
+    model's own preprocess keeps (avro is not installed here)."""
+    server = KFServer(registered_models=KFModelRepository())
+    server.register_model(RawBytesModel("TestModel"))
+    s = serve(server)
+    data = b"\x06foo\x02\x00\x02\x08pink"
+    code, hdrs, out = s.fetch("/v1/models/TestModel:predict", "POST", data, CE_HEADERS)
+    _check_ce_response(code, hdrs, out, b'{"predictions": [[12, "\\u0006"]]}')
+
+
+class FailingRepository(KFModelRepository):
+    def __init__(self, msg):
+        super().__init__(models_dir="/tmp")
+        self.msg = msg
+
+    async def load(self, name):
+        raise RuntimeError(self.msg)
+
+
+@pytest.mark.parametrize("msg", ["bad\r\nX-Injected: 1", "café ☃ unicode"])
+def test_error_reason_is_sanitised(serve, msg):
+    """A load error text with CR/LF or non-latin-1 characters still gives one
+    well-formed 500 response (no header injection, no dropped connection)."""
+    s = serve(KFServer(registered_models=FailingRepository(msg)))
+    conn = http.client.HTTPConnection("127.0.0.1", s.port, timeout=30)
+    conn.request("POST", "/v2/repository/models/m/load", body=b"")
+    r = conn.getresponse()
+    body = r.read()
+    assert r.status == 500
+    assert r.getheader("X-Injected") is None
+    assert "\n" not in r.reason and "\r" not in r.reason
+    assert msg.encode("utf-8") in body
+    # the connection is still usable
+    conn.request("GET", "/")
+    r = conn.getresponse()
+    assert r.status == 200 and r.read() == b"Alive"
+    conn.close()
