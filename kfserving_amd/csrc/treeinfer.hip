@@ -423,6 +423,7 @@ struct DeviceForest {
   uint2* rx_recs[2] = {nullptr, nullptr};
   uint32_t* rx_base = nullptr;
   uint32_t* rx_nint = nullptr;
+  int32_t* lx_stage = nullptr;   // staged record layout (7): first tree of each stage
   // TreeSHAP path tables
   ShapPath* shap_paths = nullptr;
   ShapElem* shap_elems = nullptr;
@@ -513,9 +514,14 @@ struct ti_forest {
     int32_t rows = 256;
     int32_t words = 0;
   } rx[2];
-  std::vector<uint32_t> h_rx_base, h_rx_nint;
+  std::vector<uint32_t> h_rx_base, h_rx_nint;   // h_rx_base: [T+1]
   int64_t rx_slots = 0;
   int32_t rx_ilp = 8;
+  // staged record layout (7): the same records, copied into LDS a stage of
+  // consecutive trees at a time; stage k holds trees [h_lx_stage[k], h_lx_stage[k+1])
+  std::vector<int32_t> h_lx_stage;
+  int64_t lx_stage_cap = 0;    // LDS bytes of the stage area
+  int32_t lx_ilp = 8;
   std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
   // TreeSHAP (TI_OUTPUT_CONTRIB); has_shap = 0 when the forest has no covers.
   // The path tables are built and uploaded on the first contributions call
@@ -572,7 +578,7 @@ void free_device(DeviceForest& d) {
                   d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1],
                   d.bx_nodes[0], d.bx_nodes[1], d.bx_tbl[0], d.bx_tbl[1],
                   d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias,
-                  d.rx_recs[0], d.rx_recs[1], d.rx_base, d.rx_nint};
+                  d.rx_recs[0], d.rx_recs[1], d.rx_base, d.rx_nint, d.lx_stage};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d.hx_pin) (void)hipHostFree(d.hx_pin);
@@ -609,6 +615,7 @@ void free_device(DeviceForest& d) {
   }
   d.rx_recs[0] = d.rx_recs[1] = nullptr;
   d.rx_base = d.rx_nint = nullptr;
+  d.lx_stage = nullptr;
   d.shap_paths = nullptr;
   d.shap_elems = nullptr;
   d.shap_leaf = d.shap_bias = nullptr;
@@ -1184,7 +1191,7 @@ bool pack_bexplicit(const ti_forest_desc* d, ti_forest* f, ti_forest::BinExplici
 // 65,535 nodes (16-bit child slots).
 bool plan_rx_slots(const ti_forest_desc* d, ti_forest* f, std::vector<uint32_t>* slot_of) {
   slot_of->assign(d->n_nodes, 0);
-  f->h_rx_base.assign(d->n_trees, 0);
+  f->h_rx_base.assign(d->n_trees + 1, 0);   // [T]: the slot count (staged layout)
   f->h_rx_nint.assign(d->n_trees, 0);
   if (d->n_nodes >= (int64_t(1) << 31)) return false;
   std::vector<int32_t> q;
@@ -1209,6 +1216,7 @@ bool plan_rx_slots(const ti_forest_desc* d, ti_forest* f, std::vector<uint32_t>*
     }
     f->h_rx_nint[t] = n_int;
   }
+  f->h_rx_base[d->n_trees] = static_cast<uint32_t>(d->n_nodes);
   f->rx_slots = d->n_nodes;
   return true;
 }
@@ -1230,7 +1238,8 @@ bool pack_rexplicit(const ti_forest_desc* d, const ti_forest* f,
   rx->rows = R;
   rx->L = rt.L;
   eytzinger_tables(rt, &rx->tbl);
-  rx->recs.assign(d->n_nodes, uint2{0u, 0u});
+  // an even slot count: the staged layout copies whole 16-byte words
+  rx->recs.assign(d->n_nodes + (d->n_nodes & 1), uint2{0u, 0u});
   const bool scalar_leaves = d->leaf_width == 1;
   for (int t = 0; t < d->n_trees; ++t) {
     const int64_t b = d->tree_offset[t];
@@ -1247,8 +1256,8 @@ bool pack_rexplicit(const ti_forest_desc* d, const ti_forest* f,
         const uint32_t rank = rt.rank(fe, d->threshold[g]);
         r.x = off | ((d->flags[g] & TI_NODE_NAN_LEFT) ? ti::kRxNanLeft : 0u);
         if (zero) {
-          r.x |= (2u * rank + 1u) << 16;
-          if (d->flags[g] & TI_NODE_ZERO_FLIP) r.x |= 0x80000000u;
+          r.x |= (2u * rank + 1u) << 16;   // <= 32,765: bit 31 stays clear
+          if (d->flags[g] & TI_NODE_ZERO_FLIP) r.x |= ti::kRxZeroFlip;
         } else {
           r.x |= rank << 16;
         }
@@ -1257,6 +1266,60 @@ bool pack_rexplicit(const ti_forest_desc* d, const ti_forest* f,
       rx->recs[b + slot_of[g]] = r;
     }
   }
+  return true;
+}
+
+// Staged record layout (7): forests whose trees are small enough that a run
+// of several consecutive trees' records fits in LDS beside the bin image walk
+// from LDS instead of gathering every node through the vector memory pipe
+// (the bound of layout 6: TD busy 92 % of the kernel, profiles/r2_c3_l6b_*).
+// The stage area is what 160 KB / TI_LX_WGS (2) workgroups per CU leave after
+// the bin image, capped by the prefetch registers (kLxPf x 16 B per thread).
+// A stage is a maximal run of consecutive trees whose records (their span
+// widened to 16-byte words) fit the area.  Returns false (layout 6 stays) when
+// fewer than two of the largest trees fit.
+constexpr int kLxPf = 8;
+// every masked bin address ((x & 0xFFFA) | lane offset <= 66,558) must stay
+// inside the workgroup's LDS allocation: leaf records hold values, not offsets
+constexpr size_t kLxMinLds = 66560;
+bool plan_lx_stages(ti_forest* f, int T) {
+  const int R = f->rx[0].rows;
+  if (f->rx[1].rows != R) return false;
+  const size_t bins = align16(static_cast<size_t>(std::max(f->rx[0].words, f->rx[1].words)) * R * 4 + 4);
+  const int wgs = std::max(1, env_int("TI_LX_WGS", 2));
+  size_t cap = kLdsPerCu / static_cast<size_t>(wgs);
+  cap = cap > bins ? cap - bins : 0;
+  cap = std::min(cap, static_cast<size_t>(kLxPf) * 16 * R) & ~size_t(15);
+  const std::vector<uint32_t>& b = f->h_rx_base;
+  auto span = [&](int t0, int t1) {
+    return ((static_cast<size_t>(b[t1]) * 8 + 15) & ~size_t(15)) - ((static_cast<size_t>(b[t0]) * 8) & ~size_t(15));
+  };
+  size_t biggest = 0;
+  for (int t = 0; t < T; ++t) biggest = std::max(biggest, span(t, t + 1));
+  if (T < 2 || cap < 2 * biggest + 16) return false;
+  f->h_lx_stage.assign(1, 0);
+  int t0 = 0;
+  while (t0 < T) {
+    int t1 = t0 + 1;
+    while (t1 < T && span(t0, t1 + 1) <= cap) ++t1;
+    f->h_lx_stage.push_back(t1);
+    t0 = t1;
+  }
+  f->lx_stage_cap = static_cast<int64_t>(cap);
+  // children as byte offsets in the tree (a stage is <= 32 KB: < 8,192 slots)
+  for (auto& rx : f->rx)
+    for (int t = 0; t < T; ++t)
+      for (uint32_t v = b[t]; v < b[t] + f->h_rx_nint[t]; ++v) {
+        uint2& r = rx.recs[v];
+        r.y = (((r.y >> 16) << 3) << 16) | ((r.y & 0xFFFFu) << 3);
+      }
+  // trees in lockstep per lane: a stage's worth when stages hold 7 or 8 trees
+  // (C3: 7 trees of 4,072 B per 30.7 KB stage; a group wider than the stage
+  // walks a duplicate tree), else 4
+  const double per_stage = static_cast<double>(T) / static_cast<double>(f->h_lx_stage.size() - 1);
+  f->lx_ilp = per_stage >= 7.5 ? 8 : per_stage >= 6.5 ? 7 : 4;
+  const int force_ilp = env_int("TI_LX_ILP", 0);
+  if (force_ilp > 0) f->lx_ilp = force_ilp >= 8 ? 8 : force_ilp == 7 ? 7 : 4;
   return true;
 }
 
@@ -1434,13 +1497,14 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
     if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
     d.leaves = lv;
     if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
-  } else if (f->layout == 6) {
+  } else if (f->layout == 6 || f->layout == 7) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.rx_recs[i], f->rx[i].recs, &d.bytes))) return rc;
       if ((rc = upload(&d.bx_tbl[i], f->rx[i].tbl, &d.bytes))) return rc;
     }
     if ((rc = upload(&d.rx_base, f->h_rx_base, &d.bytes))) return rc;
     if ((rc = upload(&d.rx_nint, f->h_rx_nint, &d.bytes))) return rc;
+    if (f->layout == 7 && (rc = upload(&d.lx_stage, f->h_lx_stage, &d.bytes))) return rc;
     if ((rc = upload(&d.leaf_base, f->h_leaf_base, &d.bytes))) return rc;
     if (f->LW > 1) {   // vector leaves are read from the leaf table
       unsigned char* lv = nullptr;
@@ -1522,6 +1586,13 @@ KernelFn select_rexplicit(int xdt, int accum, int K, bool z, int ilp) {
   return ti::kernels_df(6, K, true, z, true, ilp);
 }
 
+KernelFn select_lexplicit(int xdt, int accum, int K, bool z, int ilp) {
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(7, K, true, z, true, ilp);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(7, K, true, z, true, ilp);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(7, K, true, z, true, ilp);
+  return ti::kernels_df(7, K, true, z, true, ilp);
+}
+
 KernelFn select_sexplicit(int xdt, int accum, int K, bool b16, bool z, int ilp) {
   if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(5, K, true, z, b16, ilp);
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(5, K, true, z, b16, ilp);
@@ -1580,7 +1651,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     R = f->bh[xdt == TI_F64 ? 1 : 0].rows;
   } else if (f->layout == 4 || f->layout == 5) {
     R = f->bx[xdt == TI_F64 ? 1 : 0].rows;
-  } else if (f->layout == 6) {
+  } else if (f->layout == 6 || f->layout == 7) {
     R = f->rx[xdt == TI_F64 ? 1 : 0].rows;
   } else {
     R = 256;
@@ -1593,7 +1664,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   if (f->layout == 3) feat_bytes = static_cast<size_t>(f->bh[xdt == TI_F64 ? 1 : 0].words) * R * 4;
   if (f->layout == 4 || f->layout == 5)
     feat_bytes = static_cast<size_t>(f->bx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
-  if (f->layout == 6) feat_bytes = static_cast<size_t>(f->rx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
+  if (f->layout == 6 || f->layout == 7)
+    feat_bytes = static_cast<size_t>(f->rx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
 
   KArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1729,6 +1801,33 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.bin_words = rx.words;
     lds = feat_bytes + 16;
     KernelFn fn = select_rexplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->rx_ilp);
+    int rc = ensure_lds_attr(d.device, fn);
+    if (rc) return rc;
+    const int64_t grid = (rows + R - 1) / R;
+    if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    TI_HIP(hipGetLastError());
+    return TI_OK;
+  } else if (f->layout == 7) {
+    const int ii = xdt == TI_F64 ? 1 : 0;
+    const ti_forest::RecExplicit& rx = f->rx[ii];
+    a.rx_recs = d.rx_recs[ii];
+    a.rx_base = d.rx_base;
+    a.rx_nint = d.rx_nint;
+    a.leaf_base = d.leaf_base;
+    a.rx_slots = static_cast<uint32_t>(f->rx_slots);
+    a.leaves = d.leaves;
+    a.exp_leaf_ids = d.exp_leaf_ids;
+    a.bin_tbl = d.bx_tbl[ii];
+    a.bin_L = rx.L;
+    a.bin_words = rx.words;
+    a.stage_start = d.lx_stage;
+    a.n_stages = static_cast<int32_t>(f->h_lx_stage.size() - 1);
+    a.stage_off = static_cast<int32_t>(align16(feat_bytes + 4));
+    lds = std::max(static_cast<size_t>(a.stage_off) + static_cast<size_t>(f->lx_stage_cap), kLxMinLds);
+    if (lds > kLdsPerCu || static_cast<int64_t>(kLxPf) * 16 * R < f->lx_stage_cap)
+      return fail(TI_ERR_UNSUPPORTED, "staged record layout exceeds LDS");
+    KernelFn fn = select_lexplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -2408,7 +2507,8 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   bool use_compact = false;
   if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
   if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
-  if (want == "explicit" || want == "bexplicit" || want == "sexplicit" || want == "rexplicit") {
+  if (want == "explicit" || want == "bexplicit" || want == "sexplicit" || want == "rexplicit" ||
+      want == "lexplicit") {
     use_heap = false;
     use_compact = false;
   }
@@ -2496,6 +2596,10 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         f->rx_ilp = md < 12.0 ? 16 : 8;
         const int force_ilp = env_int("TI_RX_ILP", 0);
         if (force_ilp > 0) f->rx_ilp = force_ilp >= 16 ? 16 : force_ilp >= 8 ? 8 : 4;
+        // small trees: staged in LDS (layout 7) unless layout 6 is forced
+        if (want != "rexplicit" && env_int("TI_NO_LEXPLICIT", 0) == 0 &&
+            plan_lx_stages(f.get(), f->T))
+          f->layout = 7;
       } else {
         for (auto& rx : f->rx) rx = ti_forest::RecExplicit();
         f->h_rx_base.clear();

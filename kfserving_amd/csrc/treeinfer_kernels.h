@@ -1263,8 +1263,14 @@ __global__ void __launch_bounds__(256) sexplicit_predict_kernel(const KArgs a) {
 //   right = (rank < b) ^ (b == kNan && NaN-left)
 // LightGBM zero-missing forests (ZERO) bin as b2 = 2 b + (x == 0) with NaN =
 // 0xFFFE and store rank2 = 2 rank + 1 (rank2 < b2 <=> rank < b, exactly) and
-// the zero flip in x bit 31:  right ^= (b2 odd) && zero-flip.
+// the zero flip in x bit 2 (the bin offset's lane part, clear in the record):
+//   right ^= (b2 odd) && zero-flip.
+// A tile whose rows hold no NaN (and, for ZERO, no exact 0 after LightGBM's
+// zero map) needs neither term: b2 is even there, so the step is the plain
+// rank compare on x's high half for every forest (rx_next_fast, 2 VALU).
 constexpr uint32_t kRxNanLeft = 1u;
+constexpr uint32_t kRxZeroFlip = 4u;
+constexpr uint32_t kRxOffMask = 0xFFFAu;   // the bin byte offset without the flag bits
 
 // Slot loads are structured buffer loads: vindex = the slot (VGPR), soffset =
 // the tree's first byte (wave-uniform SGPR), stride 8 in the resource, so the
@@ -1285,70 +1291,42 @@ __device__ __forceinline__ rx_rsrc_t rx_make_rsrc(const void* base, uint32_t n_s
   return r;
 }
 
-// One split decision, hand-scheduled: the rank compare on the record's high
-// half, the flips, then the child slot picked from the two halves of y by
-// one SDWA select on the compare's mask.
-template <bool ZERO, bool CHECK_NAN>
-__device__ __forceinline__ uint32_t rx_next(uint32_t x, uint32_t y, uint32_t b) {
+// One split decision.  The fast form (tiles without NaN / exact zeros) is the
+// rank compare of the record's high half with the bin and one SDWA select of
+// the child from the two halves of y on the compare's mask: 2 VALU.  The bin
+// comes straight from ds_read_u16 as a 16-bit value; the compare reads its low
+// word (src1_sel:WORD_0), so no zero-extension is spent on it.  The slow form
+// adds the zero flip and the NaN direction (rare tiles; compiler-scheduled).
+__device__ __forceinline__ uint32_t rx_next_fast(uint32_t x, uint32_t y, uint16_t b) {
   uint32_t slot;
-  if (!ZERO && !CHECK_NAN) {
-    asm("v_cmp_lt_u32_sdwa vcc, %1, %3 src0_sel:WORD_1 src1_sel:DWORD\n\t"
-        "v_cndmask_b32_sdwa %0, %2, %2, vcc src0_sel:WORD_0 src1_sel:WORD_1"
-        : "=v"(slot) : "v"(x), "v"(y), "v"(b) : "vcc");
-  } else if (!ZERO) {
-    uint64_t n, m;
-    uint32_t t;
-    asm("v_cmp_lt_u32_sdwa vcc, %4, %6 src0_sel:WORD_1 src1_sel:DWORD\n\t"
-        "v_cmp_eq_u32_e64 %1, %7, %6\n\t"
-        "v_and_b32 %3, 1, %4\n\t"
-        "v_cmp_ne_u32_e64 %2, 0, %3\n\t"
-        "s_and_b64 %1, %1, %2\n\t"
-        "s_xor_b64 vcc, vcc, %1\n\t"
-        "v_cndmask_b32_sdwa %0, %5, %5, vcc src0_sel:WORD_0 src1_sel:WORD_1"
-        : "=v"(slot), "=&s"(n), "=&s"(m), "=&v"(t)
-        : "v"(x), "v"(y), "v"(b), "s"(0xFFFFu)
-        : "vcc", "scc");
-  } else {
-    // rank2 = x bits 16..30; zero flip = x bit 31 (x < 0 as i32); b2 odd = exact 0
-    uint64_t z, w, n, m;
-    uint32_t r, t;
-    if (!CHECK_NAN) {
-      asm("v_bfe_u32 %3, %5, 16, 15\n\t"
-          "v_cmp_lt_u32_e32 vcc, %3, %7\n\t"
-          "v_and_b32 %4, 1, %7\n\t"
-          "v_cmp_ne_u32_e64 %1, 0, %4\n\t"
-          "v_cmp_gt_i32_e64 %2, 0, %5\n\t"
-          "s_and_b64 %1, %1, %2\n\t"
-          "s_xor_b64 vcc, vcc, %1\n\t"
-          "v_cndmask_b32_sdwa %0, %6, %6, vcc src0_sel:WORD_0 src1_sel:WORD_1"
-          : "=v"(slot), "=&s"(z), "=&s"(w), "=&v"(r), "=&v"(t)
-          : "v"(x), "v"(y), "v"(b)
-          : "vcc", "scc");
-    } else {
-      asm("v_bfe_u32 %5, %7, 16, 15\n\t"
-          "v_cmp_lt_u32_e32 vcc, %5, %9\n\t"
-          "v_and_b32 %6, 1, %9\n\t"
-          "v_cmp_ne_u32_e64 %1, 0, %6\n\t"
-          "v_cmp_gt_i32_e64 %2, 0, %7\n\t"
-          "s_and_b64 %1, %1, %2\n\t"
-          "s_xor_b64 vcc, vcc, %1\n\t"
-          "v_cmp_eq_u32_e64 %3, %10, %9\n\t"
-          "v_and_b32 %6, 1, %7\n\t"
-          "v_cmp_ne_u32_e64 %4, 0, %6\n\t"
-          "s_and_b64 %3, %3, %4\n\t"
-          "s_xor_b64 vcc, vcc, %3\n\t"
-          "v_cndmask_b32_sdwa %0, %8, %8, vcc src0_sel:WORD_0 src1_sel:WORD_1"
-          : "=v"(slot), "=&s"(z), "=&s"(w), "=&s"(n), "=&s"(m), "=&v"(r), "=&v"(t)
-          : "v"(x), "v"(y), "v"(b), "s"(0xFFFEu)
-          : "vcc", "scc");
-    }
-  }
+  asm("v_cmp_lt_u32_sdwa vcc, %1, %3 src0_sel:WORD_1 src1_sel:WORD_0\n\t"
+      "v_cndmask_b32_sdwa %0, %2, %2, vcc src0_sel:WORD_0 src1_sel:WORD_1"
+      : "=v"(slot) : "v"(x), "v"(y), "v"(b) : "vcc");
   return slot;
+}
+template <bool ZERO>
+__device__ __forceinline__ uint32_t rx_next_slow(uint32_t x, uint32_t y, uint16_t b16) {
+  constexpr uint32_t kNan = ZERO ? 0xFFFEu : 0xFFFFu;
+  const uint32_t b = b16;
+  bool right = (x >> 16) < b;
+  if (ZERO) right = right != (((b & 1u) != 0u) && ((x & kRxZeroFlip) != 0u));
+  if (b == kNan) right = (x & kRxNanLeft) == 0u;
+  return right ? (y >> 16) : (y & 0xFFFFu);
+}
+template <bool ZERO, bool SLOW>
+__device__ __forceinline__ uint32_t rx_next(uint32_t x, uint32_t y, uint16_t b) {
+  return SLOW ? rx_next_slow<ZERO>(x, y, b) : rx_next_fast(x, y, b);
+}
+__device__ __forceinline__ uint16_t lds_u16(uint32_t byte_addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(
+      static_cast<uintptr_t>(byte_addr));
 }
 
 // Bin the tile's rows (as stage_bins_rows, one lane per row, per-lane loads)
-// into the u16 image of layout 6: b = 1 + #{u < x}, NaN = 0xFFFF; with ZB
-// (zero-missing forests) b2 = 2 b + (x == 0) and NaN = 0xFFFE.
+// into the u16 image of layouts 6 / 7: b = 1 + #{u < x}, NaN = 0xFFFF; with ZB
+// (zero-missing forests) b2 = 2 b + (x == 0) and NaN = 0xFFFE.  Returns
+// (uniformly) whether the tile needs the slow step: a NaN, or with ZB an
+// exact 0.
 template <typename XT, bool ZB>
 __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
                                               int R, int tid) {
@@ -1387,9 +1365,10 @@ __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const bool nan = x[q] != x[q];
-      has_nan |= nan && (f0 + q < F);
+      const bool zero = ZB && x[q] == XT(0);
+      has_nan |= (nan || zero) && (f0 + q < F);   // the tile needs the slow step
       uint32_t b = 1u + k[q] - tsz;
-      if (ZB) b = nan ? 0xFFFEu : 2u * b + (x[q] == XT(0) ? 1u : 0u);
+      if (ZB) b = nan ? 0xFFFEu : 2u * b + (zero ? 1u : 0u);
       else b = nan ? 0xFFFFu : b;
       w[q / 2] |= b << ((q % 2) * 16);
     }
@@ -1411,24 +1390,46 @@ __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a
 }
 
 // Per step every tree's bin read is issued first, then each tree's decision
-// and its exec-masked gather: only lanes still inside the tree gather, so a
-// finished lane makes no request and keeps its record -- the leaf's value,
-// read by the gather that reached it.  The gathers carry no control flow
-// around them, so the compiler's counted waits keep all ILP in flight.
-template <typename ACC, int KMAX, bool ZERO, bool CHECK_NAN, int ILP>
+// and its exec-masked gather: only lanes still inside the tree decide and
+// gather, so a finished lane makes no request and keeps its record -- the
+// leaf's value, read by the gather that reached it.  `in` comes from the slot
+// at the start of the step (no lane-mask state is carried across iterations:
+// the compiler would rebuild every mask in every branch); the loop runs one
+// step past the group's last leaf.  A lane at its leaf reads its own column
+// of bin word 0 instead of an address made of its record's value bits: the
+// random addresses of finished lanes made 66 % of the LDS cycles bank
+// conflicts (profiles/r2_c3_l6c_pmc.json).  VIS: scalar leaf values sit in
+// the leaf records; otherwise the slot gives the leaf index.
+template <typename ACC, int KMAX>
+__device__ __forceinline__ void rx_leaves(const KArgs& a, ACC (&acc)[KMAX], int t, uint32_t slot,
+                                          uint32_t ni, uint32_t rx, uint32_t ry, int64_t row,
+                                          bool live, bool vis) {
+  const int LW = a.leaf_width;
+  if (vis) {
+    ACC v;
+    if (sizeof(ACC) == 8) v = (ACC)__hiloint2double((int)ry, (int)rx);
+    else v = (ACC)__uint_as_float(rx);
+    add_leaf<ACC, KMAX>(acc, &v, 0, 1, a.tree_group[t]);
+    return;
+  }
+  // leaf ids / vector leaves: the leaf's index from its slot
+  const int64_t li = a.leaf_base[t] + (int64_t)(slot - ni);
+  if (a.kind == TI_OUTPUT_LEAF) {
+    if (live) static_cast<int32_t*>(a.out)[row * a.n_trees + t] = a.exp_leaf_ids[li];
+  } else {
+    add_leaf<ACC, KMAX>(acc, static_cast<const ACC*>(a.leaves) + li * LW, 0, LW, a.tree_group[t]);
+  }
+}
+
+typedef const __attribute__((address_space(4))) uint32_t rx_cu32;   // scalar-loaded tables
+
+template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP>
 __device__ __forceinline__ void rx_walk(const KArgs& a, ACC (&acc)[KMAX], uint32_t lane_off,
                                         int64_t row, bool live) {
   const int T = a.n_trees;
-  const int LW = a.leaf_width;
-  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
-  const bool value_in_slot = LW == 1 && !want_leaf;
   const rx_rsrc_t rsrc = rx_make_rsrc(a.rx_recs, a.rx_slots);
-  const uint32_t bin_limit = (uint32_t)a.bin_words * blockDim.x * 4u;
-  // read-only tables addressed by wave-uniform indices: the constant address
-  // space makes these scalar loads
-  typedef const __attribute__((address_space(4))) uint32_t cu32;
-  cu32* rx_base = reinterpret_cast<cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
-  cu32* rx_nint = reinterpret_cast<cu32*>(reinterpret_cast<uintptr_t>(a.rx_nint));
+  rx_cu32* rx_base = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* rx_nint = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_nint));
   for (int t0 = 0; t0 < T; t0 += ILP) {
     uint32_t sb[ILP], ni[ILP];   // tree's first byte and internal-slot count (SGPRs)
     uint32_t slot[ILP];          // the lane's slot in each tree
@@ -1442,53 +1443,30 @@ __device__ __forceinline__ void rx_walk(const KArgs& a, ACC (&acc)[KMAX], uint32
       rec[q] = rx_struct_load(rsrc, 0u, 0u, sb[q], 0);   // the root (or a lone leaf)
     }
     for (;;) {
+      bool in[ILP];
+      uint32_t b[ILP];
       bool any = false;
 #pragma unroll
-      for (int q = 0; q < ILP; ++q) any |= slot[q] < ni[q];
-      if (__ballot(any) == 0) break;   // every lane of every tree at a leaf
-      // bins: a lane at its leaf (record = the value) reads a clamped, harmless
-      // address; the image ends at bin_limit
-      uint32_t b[ILP];
-#pragma unroll
       for (int q = 0; q < ILP; ++q) {
-        const uint32_t ad = (rec[q].x & 0xFFFEu) | lane_off;
-        b[q] = lds_bin<true>(ad < bin_limit ? ad : lane_off);
+        in[q] = slot[q] < ni[q];
+        any |= in[q];
+        // a lane at its leaf reads its own column of word 0 (conflict-free)
+        b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
       }
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
-        const bool in = slot[q] < ni[q];
-        const uint32_t nx = rx_next<ZERO, CHECK_NAN>(rec[q].x, rec[q].y, b[q]);
-        slot[q] = in ? nx : slot[q];
-        // only lanes still inside the tree gather (exec-masked: a finished
-        // lane makes no request and keeps its record, the leaf value)
-        if (in) rec[q] = rx_struct_load(rsrc, nx, 0u, sb[q], 0);
-      }
-    }
-    if (value_in_slot) {
-#pragma unroll
-      for (int q = 0; q < ILP; ++q) {
-        if (t0 + q < T) {
-          ACC v;
-          if (sizeof(ACC) == 8) v = (ACC)__hiloint2double((int)rec[q].y, (int)rec[q].x);
-          else v = (ACC)__uint_as_float(rec[q].x);
-          add_leaf<ACC, KMAX>(acc, &v, 0, 1, a.tree_group[t0 + q]);
+        const uint32_t nx = rx_next<ZERO, SLOW>(rec[q].x, rec[q].y, (uint16_t)b[q]);
+        if (in[q]) {
+          slot[q] = nx;
+          rec[q] = rx_struct_load(rsrc, nx, 0u, sb[q], 0);
         }
       }
-    } else {
-      // leaf ids / vector leaves: the leaf's index from its slot
-#pragma unroll
-      for (int q = 0; q < ILP; ++q) {
-        if (t0 + q < T) {
-          const int64_t li = a.leaf_base[t0 + q] + (int64_t)(slot[q] - ni[q]);
-          if (want_leaf) {
-            if (live) static_cast<int32_t*>(a.out)[row * T + t0 + q] = a.exp_leaf_ids[li];
-          } else {
-            add_leaf<ACC, KMAX>(acc, static_cast<const ACC*>(a.leaves) + li * LW, 0, LW,
-                                a.tree_group[t0 + q]);
-          }
-        }
-      }
+      if (__ballot(any) == 0) break;   // every lane of every tree was at a leaf
     }
+#pragma unroll
+    for (int q = 0; q < ILP; ++q)
+      if (t0 + q < T)
+        rx_leaves<ACC, KMAX>(a, acc, t0 + q, slot[q], ni[q], rec[q].x, rec[q].y, row, live, VIS);
   }
 }
 
@@ -1501,14 +1479,133 @@ __global__ void __launch_bounds__(256) rexplicit_predict_kernel(const KArgs a) {
   const int64_t row = row0 + tid;
   const bool live = row < a.n_rows;
   volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
-  const bool tile_nan = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid);
+  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid);
   const uint32_t lane_off = (uint32_t)tid * 4u;
   ACC acc[KMAX];
   init_acc(acc, a);
-  if (tile_nan)
-    rx_walk<ACC, KMAX, ZERO, true, ILP>(a, acc, lane_off, row, live);
-  else
-    rx_walk<ACC, KMAX, ZERO, false, ILP>(a, acc, lane_off, row, live);
+  const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
+  if (slow) {
+    if (vis) rx_walk<ACC, KMAX, ZERO, true, true, ILP>(a, acc, lane_off, row, live);
+    else rx_walk<ACC, KMAX, ZERO, true, false, ILP>(a, acc, lane_off, row, live);
+  } else {
+    if (vis) rx_walk<ACC, KMAX, ZERO, false, true, ILP>(a, acc, lane_off, row, live);
+    else rx_walk<ACC, KMAX, ZERO, false, false, ILP>(a, acc, lane_off, row, live);
+  }
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
+// ---- staged record explicit (layout 7) -------------------------------------
+// Layout 6's records, walked from LDS: the workgroup copies a stage -- a run
+// of consecutive trees, the 16-byte words spanning their records -- into LDS
+// (global -> registers while the previous stage is walked, then one commit
+// between two barriers), and the lanes walk it ILP trees at a time in
+// lockstep.  A step is one ds_read_u16 (bin) and one ds_read_b64 (record)
+// per tree instead of a 64-lane gather through the vector memory pipe.  The
+// LDS allocation is at least kLxMinLds (host), so the bin read of a lane at
+// its leaf -- an address made of value bits -- stays inside it unclamped.
+__device__ __forceinline__ rx_u2_t lx_rec(uint32_t byte_addr) {
+  const uint64_t v = *reinterpret_cast<const __attribute__((address_space(3))) uint64_t*>(
+      static_cast<uintptr_t>(byte_addr));
+  rx_u2_t r;
+  r.x = (uint32_t)v;
+  r.y = (uint32_t)(v >> 32);
+  return r;
+}
+
+// Layout 7 records are layout 6's with the children as byte offsets in the
+// tree (slot x 8; trees of <= 8,191 slots), so a child's LDS address is one
+// add to the tree's base.  The step is branch-free: a lane at its leaf keeps
+// its byte offset and re-reads its leaf record, and reads its own column of
+// bin word 0 (conflict-free) instead of an address made of value bits.  (Exec-
+// masking the record reads instead, as layout 6 masks its gathers, measured
+// 8.4 vs 6.5 ms on C3: the branches cost the compiler's counted LDS waits.)
+template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP>
+__device__ __forceinline__ void lx_stage(const KArgs& a, ACC (&acc)[KMAX], int t0, int t1,
+                                         uint32_t sbase, uint32_t lane_off, int64_t row,
+                                         bool live) {
+  rx_cu32* rx_base = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* rx_nint = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_nint));
+  for (int j = t0; j < t1; j += ILP) {
+    uint32_t base[ILP], ni8[ILP], at[ILP];   // tree base (LDS), internal bytes, lane's byte
+    rx_u2_t rec[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = (j + q) < t1 ? (j + q) : (t1 - 1);
+      base[q] = sbase + (rx_base[tq] << 3);
+      ni8[q] = rx_nint[tq] << 3;
+      at[q] = 0u;
+      rec[q] = lx_rec(base[q]);
+    }
+    for (;;) {
+      bool in[ILP];
+      uint32_t b[ILP];
+      bool any = false;
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        in[q] = at[q] < ni8[q];
+        any |= in[q];
+        b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
+      }
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        const uint32_t nx = rx_next<ZERO, SLOW>(rec[q].x, rec[q].y, (uint16_t)b[q]);
+        at[q] = in[q] ? nx : at[q];
+        rec[q] = lx_rec(base[q] + at[q]);
+      }
+      if (__ballot(any) == 0) break;
+    }
+#pragma unroll
+    for (int q = 0; q < ILP; ++q)
+      if (j + q < t1)
+        rx_leaves<ACC, KMAX>(a, acc, j + q, at[q] >> 3, ni8[q] >> 3, rec[q].x, rec[q].y, row, live,
+                             VIS);
+  }
+}
+
+template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
+__global__ void __launch_bounds__(256) lexplicit_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int PF = 8;   // = kLxPf (host): a stage is at most PF x 16 B x R
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  u32x4* stage = reinterpret_cast<u32x4*>(smem + a.stage_off);
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  rx_cu32* rx_base = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* sst = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.stage_start));
+  const unsigned char* recs = reinterpret_cast<const unsigned char*>(a.rx_recs);
+  const int NS = a.n_stages;
+  // a stage's span: the 16-byte words from its first tree's slot 0 to the
+  // end of its last tree
+  auto lo_of = [&](int s) { return (rx_base[sst[s]] << 3) & ~15u; };
+  auto n16_of = [&](int s) { return (int)((((rx_base[sst[s + 1]] << 3) + 15u) & ~15u) - lo_of(s)) >> 4; };
+  u32x4 pf[PF];
+  prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(recs + lo_of(0)), n16_of(0), tid, R);
+  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid);
+  const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
+  ACC acc[KMAX];
+  init_acc(acc, a);
+  for (int s = 0; s < NS; ++s) {
+    const int t0 = (int)sst[s], t1 = (int)sst[s + 1];
+    const uint32_t lo = lo_of(s);
+    __syncthreads();   // the previous stage's walk is over
+    commit_n<PF>(pf, stage, n16_of(s), tid, R);
+    __syncthreads();
+    const int sn = s + 1 < NS ? s + 1 : s;
+    prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(recs + lo_of(sn)), n16_of(sn), tid, R);
+    const uint32_t sbase = (uint32_t)a.stage_off - lo;   // LDS address = sbase + record byte
+    if (slow) {
+      if (vis) lx_stage<ACC, KMAX, ZERO, true, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+      else lx_stage<ACC, KMAX, ZERO, true, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+    } else {
+      if (vis) lx_stage<ACC, KMAX, ZERO, false, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+      else lx_stage<ACC, KMAX, ZERO, false, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+    }
+  }
   if (!live || a.kind == TI_OUTPUT_LEAF) return;
   finish_row<ACC, KMAX>(acc, a, row);
 }

@@ -4,7 +4,7 @@ on 1M-row device batches, for several (layout, ILP) settings.  Every setting
 is checked bit for bit against the first one's output.  One JSON line each.
 
 Usage: python scripts/explicit_sweep.py [--configs c3,c4] [--rows N]
-       [--settings "bexplicit:8,rexplicit:4,rexplicit:8,rexplicit:16"]
+       [--settings "rexplicit:16,lexplicit:8,lexplicit:4,rexplicit:8"]
 """
 import argparse
 import json
@@ -40,7 +40,7 @@ def main():
     p.add_argument("--rows", type=int, default=1_000_000)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--nan", type=float, default=0.0)
-    p.add_argument("--settings", default="bexplicit:8,rexplicit:4,rexplicit:8,rexplicit:16")
+    p.add_argument("--settings", default="rexplicit:16,lexplicit:8,lexplicit:4,rexplicit:8")
     a = p.parse_args()
     import torch
     from bench_configs import device_normal, time_device
@@ -55,10 +55,14 @@ def main():
             X[torch.rand(X.shape, generator=g, device="cuda") < a.nan] = float("nan")
         ref = None
         for s in a.settings.split(","):
-            lay, ilp = s.split(":")
+            lay, ilp, *extra = s.split(":")
+            for kv in extra:   # per-setting env knobs, e.g. lexplicit:8:TI_LX_WGS=3
+                k, v = kv.split("=")
+                os.environ[k] = v
             os.environ["TI_FORCE_LAYOUT"] = lay
             os.environ["TI_RX_ILP"] = ilp
             os.environ["TI_BEXP_ILP"] = ilp
+            os.environ["TI_LX_ILP"] = ilp
             dev = DeviceForest(f, [0])
             out = torch.empty(a.rows, dtype=torch.float64, device="cuda")
             step_s, kms = time_device(dev, X, out, a.rows, F, OUT_MARGIN, TI_F32, a.steps, 1)
@@ -66,10 +70,12 @@ def main():
             if ref is None:
                 ref = o
             print(json.dumps({"config": c, "layout": lay, "got_layout": dev.info()["layout"],
-                              "ilp": int(ilp), "rows": a.rows, "nan": a.nan, "kernel_ms": kms,
+                              "ilp": int(ilp), "env": extra, "rows": a.rows, "nan": a.nan, "kernel_ms": kms,
                               "rows_per_s": a.rows / (kms * 1e-3),
                               "same_as_first": bool(np.array_equal(o, ref))}), flush=True)
             dev.close()
+            for kv in extra:
+                del os.environ[kv.split("=")[0]]
         del X
 
 

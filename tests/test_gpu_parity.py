@@ -341,11 +341,11 @@ def _dev_with_layout(forest, layout):
 
 
 LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2, "bheap": 3, "bexplicit": 4, "sexplicit": 5,
-             "rexplicit": 6}
+             "rexplicit": 6, "lexplicit": 7}
 
 
 @pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit", "rexplicit"])
+                                    "sexplicit", "rexplicit", "lexplicit"])
 def test_xgb_golden_every_layout(golden, layout):
     g = np.load(os.path.join(golden, "xgb_synth.npz"))
     trees, ti = xf.synthetic_complete_trees(40, 8, 28, seed=1)
@@ -361,7 +361,7 @@ def test_xgb_golden_every_layout(golden, layout):
     np.testing.assert_allclose(dev3.predict(g["X"], OUT_PREDICT), g["prob3"], rtol=RTOL)
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit"])
+@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit", "lexplicit"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
     g = np.load(os.path.join(golden, "lgb_synth.npz"))
@@ -379,7 +379,7 @@ def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
 
 
 @pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit", "rexplicit"])
+                                    "sexplicit", "rexplicit", "lexplicit"])
 def test_lgb_iris_fixture_every_layout(golden, layout):
     from sklearn.datasets import load_iris
     path = os.path.join(golden, "lgb_iris_v3.txt")
@@ -389,7 +389,7 @@ def test_lgb_iris_fixture_every_layout(golden, layout):
     assert np.array_equal(dev.predict(X, OUT_MARGIN), lgb_ref.predict(m, X, raw_score=True))
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit"])
+@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit", "lexplicit"])
 def test_sklearn_classifier_every_layout(golden, layout):
     fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
     gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
@@ -421,7 +421,7 @@ def test_compact_ragged_and_specials(rows):
                           port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
 
 
-@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit", "rexplicit"])
+@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit", "rexplicit", "lexplicit"])
 @pytest.mark.parametrize("rows", [1, 255, 257, 3000])
 def test_bexplicit_zero_missing_and_specials(rows, layout):
     """Binned explicit kernels (nodes in global memory / staged in LDS) on
@@ -444,6 +444,39 @@ def test_bexplicit_zero_missing_and_specials(rows, layout):
     X32 = X.astype(np.float32)
     assert np.array_equal(dev.predict(X32, OUT_MARGIN),
                           port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
+
+
+@pytest.mark.parametrize("layout", ["rexplicit", "lexplicit"])
+@pytest.mark.parametrize("special", ["nan", "zero", "tiny", "none"])
+def test_record_layouts_fast_and_slow_tiles(layout, special):
+    """Layouts 6 / 7 walk tiles without NaN (and, for zero-missing forests,
+    without exact zeros) with the 2-VALU rank step and the rest with the full
+    rule: specials confined to a few rows put both kinds of tile in one batch,
+    and every tile must agree with the C port bit for bit."""
+    trees = lf.synthetic_leafwise_trees(45, 255, 40, seed=11)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, 40, "binary sigmoid:1")
+        f = load_lightgbm_model(p)
+    dev = _dev_with_layout(f, layout)
+    assert dev.info()["layout"] == LAYOUT_ID[layout]
+    rng = np.random.default_rng(17)
+    X = rng.standard_normal((2000, 40))
+    v = {"nan": np.nan, "zero": 0.0, "tiny": 1e-36, "none": None}[special]
+    if v is not None:
+        X[700:705, rng.integers(0, 40, 5)] = v   # tile 2 (256-row tiles) only
+        X[1999, 3] = v                           # and the ragged last tile
+    want = port.lgb_predict_raw(trees, 1, 40, X)[:, 0]
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), want)
+    X32 = X.astype(np.float32)
+    assert np.array_equal(dev.predict(X32, OUT_MARGIN),
+                          port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
+    # a forest without zero-missing nodes (XGBoost): NaN tiles only
+    xt, xti = xf.synthetic_complete_trees(30, 9, 40, seed=4)
+    xfo = xf.forest_from_raw_trees(xt, xti, 40, 0, 0.0, "binary:logistic")
+    dx = _dev_with_layout(xfo, layout)
+    assert dx.info()["layout"] == LAYOUT_ID[layout]
+    assert np.array_equal(dx.predict(X32, OUT_MARGIN), port.xgb_predict(xt, xti, 1, 0.0, 40, X32)[:, 0])
 
 
 # ------------------------------------------------- sklearn GradientBoosting
