@@ -24,7 +24,9 @@ Also reported (rank 0):
                   sharded over the ranks (strong scaling, max-over-ranks wall):
                   C3 LightGBM leaf-wise 1000 x 255 leaves, F = 100, 100M rows;
                   C4 sklearn RandomForestRegressor 200 x depth 16, F = 64, 10M
-                  rows (the cached fit of scripts/make_c4_model.py).
+                  rows (the cached fit of scripts/make_c4_model.py).  Each
+                  carries a `roofline` (config_roofline): the busiest of VALU
+                  issue, LDS array and TD cycles, from a committed PMC pass.
   batched_latency, nan_variant -- see the functions below.
 """
 from __future__ import annotations
@@ -184,6 +186,40 @@ def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str):
     return out
 
 
+CUS = 256
+
+
+def config_roofline(kernel_ms: float, rows: int, layout: str, workload: str, pmc_path: str):
+    """Binding-resource roofline of a C3 / C4 launch from a committed PMC pass of
+    the same kernel at 1M rows (scripts/r2_cfgprof.sh -> scripts/make_cfg_pmc_json.py),
+    scaled by rows.  Three issue-type resources are priced, each against its
+    own peak: VALU issue (wave64 instructions, 4 cycles each, 1,024 SIMDs),
+    the LDS array (cycles, one array per CU) and the TD (vector-memory data
+    path, busy cycles per CU: what a node gather occupies).  `bound` is the
+    busiest of the three; the HBM compulsory rate is reported beside it."""
+    try:
+        with open(pmc_path) as fh:
+            pmc = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if pmc.get("workload") != workload or pmc.get("layout") != layout:
+        return None       # a pass of another kernel does not describe this one
+    t = kernel_ms * 1e-3
+    scale = rows / pmc["rows"]
+    fr = {"valu_issue": pmc["valu_insts_per_launch"] * scale * VALU_CYCLES / (SIMDS * CLOCK_HZ * t)}
+    if pmc.get("lds_idx_active_per_launch"):
+        fr["lds_array"] = pmc["lds_idx_active_per_launch"] * scale / (CUS * CLOCK_HZ * t)
+    if pmc.get("td_busy_per_launch"):
+        fr["td_busy"] = pmc["td_busy_per_launch"] * scale / (CUS * CLOCK_HZ * t)
+    bound = max(fr, key=fr.get)
+    out = {"bound": bound, "frac": fr[bound], "fracs": fr,
+           "basis": "per-row counts of the PMC pass x rows / (resource peak x kernel time)",
+           "pmc_source": pmc.get("source"), "pmc_rows": pmc["rows"]}
+    if pmc.get("hbm_bytes_per_launch"):
+        out["traffic"] = pmc["hbm_bytes_per_launch"] * scale
+    return out
+
+
 def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5, seed=7,
                     freeze_gc=True):
     """C5-style leg: open-loop Poisson arrivals of requests of
@@ -321,7 +357,7 @@ def c4_forest():
 
 
 def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_sync,
-               make_engine, cpu_fn=None):
+               make_engine, cpu_fn=None, pmc_workload=None, pmc_path=None):
     """Strong scaling: this rank's block of the batch, K steps, max-over-ranks wall."""
     import torch
     from kfserving_amd.forest import OUT_PREDICT, TI_F32
@@ -350,6 +386,8 @@ def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_
                "layout": LAYOUT_NAMES.get(eng.info()["layout"]),
                "compulsory_GBps": ((4 * n_feat + out.element_size()) * rows / (kms * 1e-3) / 1e9
                                    if kms else None)}
+        if pmc_path and kms:
+            res["roofline"] = config_roofline(kms, rows, res["layout"], pmc_workload, pmc_path)
         if cpu_fn is not None and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_fn(X[:min(rows, 20_000)].cpu().numpy())
     del X, out
@@ -464,14 +502,16 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
         if name == "c3":
             f3, t3, src = c3_forest()
             r = run_config(f3, 100, args.rows3, 3, args, world, rank, device, dev_sync,
-                           make_engine, c3_cpu(t3))
+                           make_engine, c3_cpu(t3), "c3",
+                           os.path.join(ROOT, "profiles", "r2_c3_pmc.json"))
             if r is not None:
                 r.update(config="C3 LightGBM leaf-wise 1000 trees x 255 leaves, 100 features, "
                                 "float32 input, float64 sigmoid of the raw score", model=src)
         elif name == "c4":
             f4, raw4, src = c4_forest()
             r = run_config(f4, 64, args.rows4, 2, args, world, rank, device, dev_sync,
-                           make_engine, c4_cpu(raw4))
+                           make_engine, c4_cpu(raw4), "c4",
+                           os.path.join(ROOT, "profiles", "r2_c4_pmc.json"))
             if r is not None:
                 r.update(config="C4 sklearn RandomForestRegressor 200 trees max_depth 16, "
                                 "64 features, float32 input, float64 mean", model=src)

@@ -16,5 +16,5 @@ prof() {  # out settings
   run pmc_b --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_LDS_MEM_VIOLATIONS SQ_LDS_ADDR_CONFLICT GRBM_GUI_ACTIVE || return 1
   run pmc_c --pmc SQ_INST_LEVEL_LDS SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_LDS_UNALIGNED_STALL SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM || return 1
 }
-prof r2_c3_l7 lexplicit:8 || exit 1
-prof r2_c3_l6c rexplicit:16 || exit 1
+prof r2_c3_l7b lexplicit:7 || exit 1
+
