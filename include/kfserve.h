@@ -36,6 +36,20 @@ extern "C" {
 int kf_parse_instances(const char* body, int64_t len, double* out, int64_t cap,
                        int64_t* rows, int64_t* cols);
 
+/* kf_parse_instances on `threads` host threads for bodies of at least
+ * KF_MT_MIN_BYTES (smaller bodies, or threads <= 1, take the one-thread
+ * parser).  Same contract and results, bit for bit: the rows region is cut into
+ * byte slices, each thread counts the row starts ('[') in its slice, a prefix
+ * sum gives every slice its first row, and each thread parses the rows that
+ * start in its slice straight into their place in `out`.  A slice whose rows
+ * do not end exactly where the next slice's first row begins (a missing or
+ * extra comma, ragged rows, anything outside the subset) makes the whole call
+ * return KF_FALLBACK.  Replaces the same json.loads + list conversion as
+ * kf_parse_instances, for large batch bodies. */
+#define KF_MT_MIN_BYTES (1 << 20)
+int kf_parse_instances_mt(const char* body, int64_t len, double* out, int64_t cap,
+                          int64_t* rows, int64_t* cols, int32_t threads);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

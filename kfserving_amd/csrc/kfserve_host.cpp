@@ -16,6 +16,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "kfserve.h"
 #include "pow5_table.h"
@@ -306,4 +308,141 @@ extern "C" int kf_parse_instances(const char* body, int64_t len, double* out, in
   *rows = r;
   *cols = c;
   return overflow ? KF_ERR_SPACE : KF_PARSED;
+}
+
+namespace {
+
+// One row "[n, n, ...]" at sc.p: exactly want values into dst.
+bool parse_row(Scanner& sc, double* dst, int64_t want) {
+  if (!sc.eat('[')) return false;
+  sc.ws();
+  if (sc.p < sc.end && *sc.p == ']') return false;   // empty row
+  int64_t k = 0;
+  for (;;) {
+    sc.ws();
+    double v;
+    if (k >= want || !sc.number(&v)) return false;   // too many values / not a number
+    dst[k++] = v;
+    sc.ws();
+    if (sc.eat(',')) continue;
+    if (sc.eat(']')) break;
+    return false;
+  }
+  return k == want;
+}
+
+int64_t count_rows(const char* a, const char* b) {   // '[' = a row start in the rows region
+  int64_t n = 0;
+  while (a < b && (a = static_cast<const char*>(std::memchr(a, '[', static_cast<size_t>(b - a))))) {
+    ++n;
+    ++a;
+  }
+  return n;
+}
+
+const char* next_row(const char* a, const char* b) {
+  const char* q = a < b ? static_cast<const char*>(std::memchr(a, '[', static_cast<size_t>(b - a)))
+                        : nullptr;
+  return q ? q : b;
+}
+
+}  // namespace
+
+extern "C" int kf_parse_instances_mt(const char* body, int64_t len, double* out, int64_t cap,
+                                     int64_t* rows, int64_t* cols, int32_t threads) {
+  if (!body || len < 0 || !rows || !cols) return KF_FALLBACK;
+  if (threads <= 1 || len < KF_MT_MIN_BYTES) return kf_parse_instances(body, len, out, cap, rows, cols);
+  *rows = 0;
+  *cols = 0;
+  // the envelope: {"instances": [ ... ] } with whitespace anywhere
+  Scanner sc{body, body + len};
+  sc.ws();
+  if (!sc.eat('{')) return KF_FALLBACK;
+  sc.ws();
+  if (!sc.lit("\"instances\"", 11)) return KF_FALLBACK;
+  sc.ws();
+  if (!sc.eat(':')) return KF_FALLBACK;
+  sc.ws();
+  if (!sc.eat('[')) return KF_FALLBACK;
+  sc.ws();
+  const char* p0 = sc.p;                             // the first row's '['
+  const char* e = body + len;
+  auto is_ws = [](char ch) { return ch == ' ' || ch == '\t' || ch == '\n' || ch == '\r'; };
+  while (e > p0 && is_ws(e[-1])) --e;
+  if (e <= p0 || e[-1] != '}') return KF_FALLBACK;
+  --e;
+  while (e > p0 && is_ws(e[-1])) --e;
+  if (e <= p0 || e[-1] != ']') return KF_FALLBACK;
+  --e;                                               // rows region [p0, e)
+  if (p0 >= e || *p0 != '[') return KF_FALLBACK;
+  // columns from the first row
+  int64_t c = 0;
+  {
+    Scanner f{p0, e};
+    if (!f.eat('[')) return KF_FALLBACK;
+    for (;;) {
+      f.ws();
+      double v;
+      if (!f.number(&v)) return KF_FALLBACK;
+      ++c;
+      f.ws();
+      if (f.eat(',')) continue;
+      if (f.eat(']')) break;
+      return KF_FALLBACK;
+    }
+  }
+  const int T = threads;
+  std::vector<const char*> b(static_cast<size_t>(T) + 1);
+  for (int i = 0; i <= T; ++i) b[i] = p0 + (e - p0) * i / T;
+  std::vector<int64_t> n_rows(T, 0), r0(static_cast<size_t>(T) + 1, 0);
+  std::vector<int> ok(T, 0);
+  {
+    std::vector<std::thread> th;
+    for (int i = 0; i < T; ++i)
+      th.emplace_back([&, i] { n_rows[i] = count_rows(b[i], b[i + 1]); });
+    for (auto& t : th) t.join();
+  }
+  for (int i = 0; i < T; ++i) r0[i + 1] = r0[i] + n_rows[i];
+  const int64_t R = r0[T];
+  if (R * c > cap) {
+    *rows = R;
+    *cols = c;
+    return KF_ERR_SPACE;
+  }
+  {
+    std::vector<std::thread> th;
+    for (int i = 0; i < T; ++i)
+      th.emplace_back([&, i] {
+        const char* start = next_row(b[i], b[i + 1]);
+        const char* limit = i + 1 < T ? next_row(b[i + 1], e) : e;
+        if (start >= limit) {   // no row starts in this slice
+          ok[i] = n_rows[i] == 0;
+          return;
+        }
+        Scanner s{start, e};
+        int64_t r = r0[i];
+        for (;;) {
+          if (r >= r0[i + 1] || !parse_row(s, out + r * c, c)) return;
+          ++r;
+          s.ws();
+          if (s.p == e) {   // the last row of the body: no comma after it
+            ok[i] = limit == e && r == r0[i + 1];
+            return;
+          }
+          if (!s.eat(',')) return;
+          s.ws();
+          if (s.p == limit) {   // the next slice's first row
+            ok[i] = r == r0[i + 1];
+            return;
+          }
+          if (s.p > limit) return;
+        }
+      });
+    for (auto& t : th) t.join();
+  }
+  for (int i = 0; i < T; ++i)
+    if (!ok[i]) return KF_FALLBACK;
+  *rows = R;
+  *cols = c;
+  return KF_PARSED;
 }

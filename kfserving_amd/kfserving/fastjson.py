@@ -34,6 +34,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
             lib.kf_parse_instances.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p,
                                                ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
                                                ctypes.POINTER(ctypes.c_int64)]
+            lib.kf_parse_instances_mt.restype = ctypes.c_int
+            lib.kf_parse_instances_mt.argtypes = lib.kf_parse_instances.argtypes + [ctypes.c_int32]
             _lib = lib
         return _lib
 
@@ -46,13 +48,19 @@ class JsonInstances(np.ndarray):
     for an ndarray argument."""
 
 
-def parse_instances(body: bytes) -> Optional[JsonInstances]:
+# host threads for bodies of >= 1 MB (kf_parse_instances_mt); the serving box
+# gives a process a share of its cores, so a fixed small count
+PARSE_THREADS = max(1, min(8, int(os.environ.get("KF_PARSE_THREADS", "8"))))
+
+
+def parse_instances(body: bytes, threads: Optional[int] = None) -> Optional[JsonInstances]:
     lib = load_library()
     n = len(body)
+    # a number takes >= 1 byte plus a separator: (n + 1) // 2 values always fit
     out = np.empty((n + 1) // 2, dtype=np.float64)
     rows, cols = ctypes.c_int64(0), ctypes.c_int64(0)
-    rc = lib.kf_parse_instances(body, n, out.ctypes.data, out.size, ctypes.byref(rows),
-                                ctypes.byref(cols))
+    rc = lib.kf_parse_instances_mt(body, n, out.ctypes.data, out.size, ctypes.byref(rows),
+                                   ctypes.byref(cols), PARSE_THREADS if threads is None else threads)
     if rc != KF_PARSED:
         return None
     r, c = rows.value, cols.value

@@ -95,3 +95,51 @@ def test_large_body():
     X = np.random.default_rng(1).standard_normal((20000, 28))
     body = json.dumps({"instances": X.tolist()}).encode()
     assert _same(np.asarray(parse_instances(body)), X)
+
+
+# ---------------------------------------------------------------- threaded
+def _big_body(seed, rows=3000, cols=28):
+    return _body(random.Random(seed), rows, cols)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_threaded_bit_exact(seed):
+    """kf_parse_instances_mt (bodies >= 1 MB): the same matrix as json.loads
+    and the one-thread parser, for any thread count (slice cuts land anywhere:
+    inside numbers, whitespace, between rows)."""
+    body = _big_body(seed)
+    assert len(body) >= 1 << 20
+    want = _ref(body)
+    one = parse_instances(body, threads=1)
+    assert _same(np.asarray(one), want)
+    for t in (2, 3, 7, 8, 16):
+        got = parse_instances(body, threads=t)
+        assert got is not None and isinstance(got, JsonInstances), t
+        assert _same(np.asarray(got), want), t
+
+
+def test_threaded_rejects_what_one_thread_rejects():
+    """Malformed bodies fall back whichever slice the damage lands in: a
+    missing or doubled row comma, a ragged row, a stray bracket, trailing
+    junk, a broken envelope."""
+    body = _big_body(4).decode()
+    rows_at = [i for i, ch in enumerate(body) if ch == "["][2:]   # row starts after the first
+    rng = random.Random(5)
+    cases = []
+    for k in rng.sample(rows_at, 12):
+        j = body.rfind(",", 0, k)                         # the comma before this row
+        cases.append(body[:j] + body[j + 1:])             # missing comma
+        cases.append(body[:j] + ",," + body[j + 1:])      # doubled comma
+        e = body.find("]", k)
+        c = body.rfind(",", k, e)
+        cases.append(body[:c] + body[e:])                 # ragged: last value of the row dropped
+        cases.append(body[:k] + "[" + body[k:])           # stray '[' (a nested row)
+        cases.append(body[:e] + ",]" + body[e + 1:])      # trailing comma in a row
+    cases.append(body + "x")
+    cases.append(body.replace('"instances"', '"instance"', 1))
+    cases.append(body.rstrip()[:-1])                       # no closing brace
+    for bad in cases:
+        b = bad.encode()
+        assert parse_instances(b, threads=1) is None
+        for t in (2, 8):
+            assert parse_instances(b, threads=t) is None, (t, bad[:80])
