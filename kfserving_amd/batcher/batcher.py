@@ -159,6 +159,9 @@ class ModelBatcher(Batcher):
         if kind == "inputs":
             async def predict_batch(X):
                 return await call(model.predict_batched, X)
+        elif kind == "tensor":   # V2 tensors (kfserving.v2): matrices, numpy semantics
+            async def predict_batch(X):
+                return await call(model.predict_tensor_batched, X)
         else:
             async def predict_batch(instances):
                 return await call(model.predict, {"instances": instances})

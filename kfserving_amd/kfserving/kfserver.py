@@ -35,7 +35,9 @@ from concurrent.futures import ThreadPoolExecutor
 from http import HTTPStatus
 from typing import Dict, List, Optional, Tuple
 
-from . import cloudevent, fastjson
+import numpy as np
+
+from . import cloudevent, fastjson, v2
 from .errors import HTTPError
 from .kfmodel import KFModel
 from .kfmodel_repository import KFModelRepository
@@ -158,15 +160,15 @@ class Application:
             (re.compile(rf"^/v1/models/{name}$"), self.health),
             (re.compile(rf"^/v2/models/{name}/status$"), self.health),
             (re.compile(rf"^/v1/models/{name}:predict$"), self.predict),
-            (re.compile(rf"^/v2/models/{name}/infer$"), self.predict),
+            (re.compile(rf"^/v2/models/{name}/infer$"), self.infer),
             (re.compile(rf"^/v1/models/{name}:explain$"), self.explain),
             (re.compile(rf"^/v2/models/{name}/explain$"), self.explain),
             (re.compile(rf"^/v2/repository/models/{name}/load$"), self.load),
             (re.compile(rf"^/v2/repository/models/{name}/unload$"), self.unload),
         ]
         self._methods = {self.liveness: "GET", self.list_models: "GET", self.health: "GET",
-                         self.predict: "POST", self.explain: "POST", self.load: "POST",
-                         self.unload: "POST"}
+                         self.predict: "POST", self.infer: "POST", self.explain: "POST",
+                         self.load: "POST", self.unload: "POST"}
 
     async def handle(self, method: str, path: str, headers: Dict[str, str], body: bytes) -> Response:
         path = path.split("?", 1)[0]
@@ -245,6 +247,51 @@ class Application:
         request = model.preprocess(request)
         request = self.validate(request)
         return _ok(await self._predict_request(model, name, request))
+
+    async def infer(self, headers, body, name):
+        """``/v2/models/<name>/infer`` (ref kfserver.py:77-78 routes it to the
+        v1 handler).  V2 tensor bodies -- JSON ``data`` or the binary
+        tensor-data extension -- are decoded into a matrix and answered as a
+        V2 inference response (kfserving.v2); any other body takes the v1
+        path unchanged.  Malformed tensor requests get 400 with
+        ``{"error": ...}`` (required_api.md:326-340)."""
+        def bad(msg):
+            return 400, "Bad Request", {"Content-Type": "application/json"}, v2.error_body(msg)
+        try:
+            head, tail = v2.split_body(headers, body)
+        except v2.V2Error as e:
+            return bad(str(e))
+        # a tensor request names a datatype; v1 bodies skip the second decode
+        req = v2.parse_header(head) if (tail or b'"datatype"' in head) else None
+        if req is None:
+            if tail:
+                return bad("binary tensor data without a V2 inference request header")
+            return await self.predict(headers, body, name)
+        model = self.get_model(name)
+        if not getattr(model, "accepts_array_instances", False):
+            # a generic KFModel gets the request dict as the reference passes it
+            return _ok(await self._predict_request(model, name, self.validate(req)))
+        try:
+            X = v2.feature_matrix(v2.decode_inputs(req, tail))
+        except v2.V2Error as e:
+            return bad(str(e))
+        if self._batcher_factory is not None:
+            key = (name, "tensor")
+            batcher = self._batchers.get(key)
+            if batcher is None or batcher.model is not model:
+                batcher = self._batcher_factory(model, self._call, "tensor")
+                self._batchers[key] = batcher
+            response = await batcher.submit(X)
+            if response.get("predictions") is None:
+                raise HTTPError(500, response.get("message") or "Failed to predict")
+            result = np.asarray(response["predictions"])
+        else:
+            try:
+                result = await self._call(model.predict_tensor, X)
+            except Exception as e:
+                raise HTTPError(500, "Failed to predict %s" % e)
+        hdrs, payload = v2.encode_response(name, req, np.asarray(result))
+        return 200, "OK", hdrs, payload
 
     async def _predict_request(self, model, name, request):
         """predict -> postprocess, through the batcher when one is configured:

@@ -42,6 +42,16 @@ class LightGBMModel(GPUForestMixin, KFModel):
     def request_matrix(self, request: Dict) -> np.ndarray:
         return lgb_matrix_from_inputs(request["inputs"], self.feature_name())
 
+    def tensor_matrix(self, X: np.ndarray) -> np.ndarray:
+        """A V2 tensor's columns in the booster's feature order, float64 (as
+        ``Booster.predict(ndarray)`` reads them)."""
+        X = np.asarray(X, dtype=np.float64)
+        n = self._forest.n_features
+        if X.ndim != 2 or X.shape[1] != n:
+            raise ValueError("The number of features in data (%d) is not the same as it was "
+                             "in training data (%d)." % (X.shape[-1], n))
+        return X
+
     def predict(self, request: Dict) -> Dict:
         try:
             result = self.predict_matrix(self.request_matrix(request))

@@ -73,6 +73,15 @@ class SKLearnModel(GPUForestMixin, KFModel):  # pylint:disable=c-extension-no-me
                              "dtype('float32').")
         return X
 
+    def predict_tensor(self, X: np.ndarray) -> np.ndarray:
+        """A V2 tensor through the same checks and label mapping as predict."""
+        f = self._forest
+        result = self.predict_matrix(self.request_matrix({"instances": X}))
+        classes = f.meta.get("classes")
+        if classes is not None:
+            result = np.asarray(classes).take(result.astype(np.int64), axis=0)
+        return result
+
     def predict(self, request: Dict) -> Dict:
         inputs = self._array(request)
         try:

@@ -48,6 +48,22 @@ class GPUForestMixin:
     def predict_matrix(self, X: np.ndarray, kind: int = OUT_PREDICT) -> np.ndarray:
         return self.device_forest().predict(X, kind)
 
+    # V2 tensors (kfserving.v2): a [rows, features] numeric matrix, read with
+    # the numpy-argument semantics of each library (NaN = missing)
+    def tensor_matrix(self, X: np.ndarray) -> np.ndarray:
+        return X
+
+    def predict_tensor(self, X: np.ndarray) -> np.ndarray:
+        return self.predict_matrix(self.tensor_matrix(X))
+
+    def predict_tensor_batched(self, X: np.ndarray) -> Dict:
+        """KFServer's batcher, kind "tensor": one predict over the rows of
+        every V2 request of a batch."""
+        try:
+            return {"predictions": self.predict_tensor(X)}
+        except Exception as e:
+            raise Exception("Failed to predict %s" % e)
+
     def explain(self, request: Dict) -> Dict:
         """The ``:explain`` route (kfserver.py:79-82 in the reference, which
         forwards to an explainer service; kfmodel.py:106-122) answered in

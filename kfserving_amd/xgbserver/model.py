@@ -39,8 +39,17 @@ class XGBoostModel(GPUForestMixin, KFModel):
     def request_matrix(self, request: Dict) -> np.ndarray:
         instances = request["instances"]
         if isinstance(instances, np.ndarray) and not isinstance(instances, JsonInstances):
-            return instances                      # DMatrix(ndarray): NaN = missing
+            return self.tensor_matrix(instances)  # DMatrix(ndarray): NaN = missing
         return xgb_matrix_from_list(instances)    # DMatrix(list) semantics (JSON rows)
+
+    def tensor_matrix(self, X: np.ndarray) -> np.ndarray:
+        # DMatrix(ndarray) stores float32: a float64 array is rounded first
+        # (comparing the double against the split would differ from xgboost
+        # for doubles that round onto the float32 threshold)
+        X = np.asarray(X)
+        if X.ndim == 1:
+            X = X.reshape(1, -1)
+        return X if X.dtype == np.float32 else X.astype(np.float32)
 
     def predict(self, request: Dict) -> Dict:
         try:
