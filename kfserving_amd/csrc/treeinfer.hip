@@ -1023,7 +1023,10 @@ bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
   bi->b16 = m_max > 253 ? 1 : 0;
   const int P = bi->b16 ? 2 : 4;
   bi->words = (F + P - 1) / P;
-  int R = env_int("TI_BHEAP_ROWS", 512);   // 512: measured +5% over 256 at F = 28 (32 waves/CU)
+  // 512: measured +5% over 256 at F = 28 (32 waves/CU); a power of two in
+  // [64, 512], as pack_rexplicit (the lane part is OR-ed into the offset)
+  int R = 64;
+  while (R < 512 && 2 * R <= env_int("TI_BHEAP_ROWS", 512)) R *= 2;
   while (R > 64 && static_cast<int64_t>(bi->words) * R * 4 > static_cast<int64_t>(ti::kBNodeOffMask) + 1)
     R >>= 1;
   if (static_cast<int64_t>(bi->words) * R * 4 > static_cast<int64_t>(ti::kBNodeOffMask) + 1) return false;
@@ -1134,7 +1137,8 @@ bool pack_bexplicit(const ti_forest_desc* d, ti_forest* f, ti_forest::BinExplici
   bx->b16 = rt.m_max > 253 ? 1 : 0;
   const int P = bx->b16 ? 2 : 4;
   bx->words = (d->n_features + P - 1) / P;
-  int R = env_int("TI_BEXP_ROWS", 256);
+  int R = 64;   // a power of two in [64, 512], as pack_rexplicit
+  while (R < 512 && 2 * R <= env_int("TI_BEXP_ROWS", 256)) R *= 2;
   while (R > 64 && static_cast<size_t>(bx->words) * R * 4 > kFeatLdsMax) R >>= 1;
   if (static_cast<size_t>(bx->words) * R * 4 > kFeatLdsMax) return false;
   bx->rows = R;
@@ -1232,7 +1236,10 @@ bool pack_rexplicit(const ti_forest_desc* d, const ti_forest* f,
   const RankTables<XT> rt = collect_ranks<XT>(d, zero);
   if (rt.m_max > (zero ? 16382u : 65533u)) return false;
   rx->words = (d->n_features + 1) / 2;
-  int R = env_int("TI_RX_ROWS", 256);
+  // a power of two in [64, 512]: the kernels OR the lane part (tid * 4) into
+  // the feature's word offset (word * R * 4), which holds only then
+  int R = 64;
+  while (R < 512 && 2 * R <= env_int("TI_RX_ROWS", 256)) R *= 2;
   while (R > 64 && static_cast<size_t>(rx->words) * R * 4 > kFeatLdsMax) R >>= 1;
   if (static_cast<size_t>(rx->words) * R * 4 > kFeatLdsMax) return false;
   rx->rows = R;

@@ -1471,7 +1471,7 @@ __device__ __forceinline__ void rx_walk(const KArgs& a, ACC (&acc)[KMAX], uint32
 }
 
 template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
-__global__ void __launch_bounds__(256) rexplicit_predict_kernel(const KArgs a) {
+__global__ void __launch_bounds__(512) rexplicit_predict_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int R = blockDim.x;
   const int tid = threadIdx.x;
@@ -1564,7 +1564,7 @@ __device__ __forceinline__ void lx_stage(const KArgs& a, ACC (&acc)[KMAX], int t
 }
 
 template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
-__global__ void __launch_bounds__(256) lexplicit_predict_kernel(const KArgs a) {
+__global__ void __launch_bounds__(512) lexplicit_predict_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int PF = 8;   // = kLxPf (host): a stage is at most PF x 16 B x R
   const int R = blockDim.x;
