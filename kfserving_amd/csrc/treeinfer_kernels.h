@@ -45,6 +45,10 @@
 #ifndef TI_PF
 #define TI_PF 8     // 16-byte words per thread prefetched for the next tree stage
 #endif
+#ifndef TI_BIN_Q
+#define TI_BIN_Q 8   // binned heap: features binary-searched at once per lane (the temp
+                     // area holds 8 columns of a 512-row tile: more would cost LDS)
+#endif
 #ifndef TI_NT_X
 #define TI_NT_X 0   // binned staging: non-temporal (streaming) feature loads
 #endif
@@ -515,7 +519,7 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
                                            int64_t row0, int R, int tid) {
   using BT = BinTraits<B16>;
   constexpr int P = BT::P;
-  constexpr int Q = 8;   // features searched at once (a multiple of P)
+  constexpr int Q = TI_BIN_Q;   // features searched at once (a multiple of P)
   const XT* X = static_cast<const XT*>(a.X);
   const XT* tbl = static_cast<const XT*>(a.bin_tbl);
   const int F = a.n_features;
@@ -563,19 +567,19 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
     __syncthreads();
     for (int c = 0; c < kc; c += Q) {
       XT x[Q];
-      const XT* tq[Q];
+      uint32_t tq[Q];   // the feature's table (element offset, not a pointer)
       uint32_t k[Q];
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const int cc = c + q < kc ? c + q : kc - 1;
         x[q] = temp[cc * R + tid];
-        tq[q] = tbl + (size_t)(f0 + cc) * tsz;
+        tq[q] = (uint32_t)(f0 + cc) * tsz;
         k[q] = 1u;
       }
       for (int s = 0; s < L; ++s) {
         XT e[Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) e[q] = tq[q][k[q]];
+        for (int q = 0; q < Q; ++q) e[q] = tbl[tq[q] + k[q]];
 #pragma unroll
         for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
       }
@@ -1327,10 +1331,13 @@ __device__ __forceinline__ uint16_t lds_u16(uint32_t byte_addr) {
 // (zero-missing forests) b2 = 2 b + (x == 0) and NaN = 0xFFFE.  Returns
 // (uniformly) whether the tile needs the slow step: a NaN, or with ZB an
 // exact 0.
+#ifndef TI_RX_BINQ
+#define TI_RX_BINQ 16   // features searched at once per lane (independent load chains)
+#endif
 template <typename XT, bool ZB>
 __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
                                               int R, int tid) {
-  constexpr int Q = 8;
+  constexpr int Q = TI_RX_BINQ;
   const XT* tbl = static_cast<const XT*>(a.bin_tbl);
   const int F = a.n_features;
   const int FC = F < a.n_cols ? F : a.n_cols;
@@ -1343,19 +1350,19 @@ __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a
   if (tid == 0) *flag = 0;
   for (int f0 = 0; f0 < F; f0 += Q) {
     XT x[Q];
-    const XT* tq[Q];
+    uint32_t tq[Q];   // the feature's table (element offset: 32 bits, not a pointer)
     uint32_t k[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int f = f0 + q < F ? f0 + q : F - 1;
       x[q] = f0 + q < FC ? zero_map(xr[f], a.lgb_zero_map) : nan_value<XT>();
-      tq[q] = tbl + (size_t)f * tsz;
+      tq[q] = (uint32_t)f * tsz;
       k[q] = 1u;
     }
     for (int s = 0; s < L; ++s) {
       XT e[Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) e[q] = tq[q][k[q]];
+      for (int q = 0; q < Q; ++q) e[q] = tbl[tq[q] + k[q]];
 #pragma unroll
       for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
     }
