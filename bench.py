@@ -47,7 +47,8 @@ HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md)
 SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 4.0
 VALU_PEAK = SIMDS * CLOCK_HZ / VALU_CYCLES     # wave64 VALU instructions / s
 LAYOUT_NAMES = {0: "heap", 1: "explicit", 2: "compact", 3: "bheap", 4: "bexplicit",
-                5: "sexplicit", 6: "rexplicit", 7: "lexplicit"}
+                5: "sexplicit", 6: "rexplicit", 7: "lexplicit",
+                8: "hexplicit"}
 
 
 def parse_args(argv=None):

@@ -424,6 +424,7 @@ struct DeviceForest {
   uint32_t* rx_base = nullptr;
   uint32_t* rx_nint = nullptr;
   int32_t* lx_stage = nullptr;   // staged record layout (7): first tree of each stage
+  uint32_t* hx_top[2] = {nullptr, nullptr};   // heap tops of layout 8, per input dtype
   // TreeSHAP path tables
   ShapPath* shap_paths = nullptr;
   ShapElem* shap_elems = nullptr;
@@ -513,6 +514,7 @@ struct ti_forest {
     int32_t L = 0;
     int32_t rows = 256;
     int32_t words = 0;
+    std::vector<uint32_t> top;   // heap tops (layout 8): [T][2^(hx_top+1)] u32
   } rx[2];
   std::vector<uint32_t> h_rx_base, h_rx_nint;   // h_rx_base: [T+1]
   int64_t rx_slots = 0;
@@ -522,6 +524,9 @@ struct ti_forest {
   std::vector<int32_t> h_lx_stage;
   int64_t lx_stage_cap = 0;    // LDS bytes of the stage area
   int32_t lx_ilp = 8;
+  // heap top + record bottom (layout 8): the top hx_top levels of each tree
+  // staged in LDS hx_stage trees at a time, walked hx_ilp trees per lane
+  int32_t hx_top = 0, hx_stage = 0, hx_ilp = 8;
   std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
   // TreeSHAP (TI_OUTPUT_CONTRIB); has_shap = 0 when the forest has no covers.
   // The path tables are built and uploaded on the first contributions call
@@ -578,7 +583,8 @@ void free_device(DeviceForest& d) {
                   d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1],
                   d.bx_nodes[0], d.bx_nodes[1], d.bx_tbl[0], d.bx_tbl[1],
                   d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias,
-                  d.rx_recs[0], d.rx_recs[1], d.rx_base, d.rx_nint, d.lx_stage};
+                  d.rx_recs[0], d.rx_recs[1], d.rx_base, d.rx_nint, d.lx_stage,
+                  d.hx_top[0], d.hx_top[1]};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d.hx_pin) (void)hipHostFree(d.hx_pin);
@@ -616,6 +622,7 @@ void free_device(DeviceForest& d) {
   d.rx_recs[0] = d.rx_recs[1] = nullptr;
   d.rx_base = d.rx_nint = nullptr;
   d.lx_stage = nullptr;
+  d.hx_top[0] = d.hx_top[1] = nullptr;
   d.shap_paths = nullptr;
   d.shap_elems = nullptr;
   d.shap_leaf = d.shap_bias = nullptr;
@@ -1330,6 +1337,67 @@ bool plan_lx_stages(ti_forest* f, int T) {
   return true;
 }
 
+// Heap tops of layout 8 (treeinfer_kernels.h, hexplicit_predict_kernel): per
+// tree 2^(D0+1) u32 entries -- [0] unused, [1, 2^D0) the x words of layout
+// 6's records at the heap positions of the top D0 levels (padding below a
+// shallow leaf: rank 0xFFFF, NaN-left, which goes left on every bin), then at
+// [2^D0, 2^(D0+1)) the layout-6 slot where the walk continues: the node at
+// depth D0, or the leaf that ended the path above it.
+constexpr uint32_t kHxPad = 0xFFFF0000u | ti::kRxNanLeft;
+constexpr int kHxPf = 8;   // = PF of hexplicit_predict_kernel
+void pack_htop(const ti_forest_desc* d, const std::vector<uint32_t>& slot_of, int D0,
+               ti_forest::RecExplicit* rx) {
+  const size_t NE = size_t(1) << D0;
+  rx->top.assign(static_cast<size_t>(d->n_trees) * 2 * NE, 0u);
+  struct Item { int32_t v; uint32_t p; int l; };
+  std::vector<Item> st;
+  for (int t = 0; t < d->n_trees; ++t) {
+    const int64_t b = d->tree_offset[t];
+    uint32_t* top = &rx->top[static_cast<size_t>(t) * 2 * NE];
+    st.assign(1, Item{0, 1u, 0});
+    while (!st.empty()) {
+      const Item it = st.back();
+      st.pop_back();
+      const int64_t g = b + it.v;
+      if (it.l == D0) {
+        top[it.p] = slot_of[g];
+        continue;
+      }
+      const bool leaf = d->feature[g] < 0;
+      top[it.p] = leaf ? kHxPad : rx->recs[b + slot_of[g]].x;
+      st.push_back(Item{leaf ? it.v : d->left[g], 2 * it.p, it.l + 1});
+      st.push_back(Item{leaf ? it.v : d->right[g], 2 * it.p + 1, it.l + 1});
+    }
+  }
+}
+
+// Layout 8's parameters and images: the top depth D0 (TI_HX_TOP, default 8,
+// at most the forest depth), ILP trees per lane (TI_HX_ILP: 4 or 8) and the
+// stage (TI_HX_STAGE trees, default ILP; at most what the prefetch registers
+// carry and what leaves the bin image room in 160 KB).  Falls back to layout 6
+// (returns false) when even ILP tops do not fit.
+constexpr int kHxMinDepth = 12;
+bool plan_htop(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>& slot_of, int D) {
+  int D0 = env_int("TI_HX_TOP", 8);
+  D0 = std::max(1, std::min(D0, std::min(D, 12)));
+  const int ilp = env_int("TI_HX_ILP", 8) >= 8 ? 8 : 4;
+  const int R = f->rx[0].rows;
+  if (f->rx[1].rows != R) return false;
+  const size_t stride = static_cast<size_t>(8) << D0;
+  const size_t bins = align16(static_cast<size_t>(std::max(f->rx[0].words, f->rx[1].words)) * R * 4 + 4);
+  const size_t cap = std::min(static_cast<size_t>(kHxPf) * 16 * R, kLdsPerCu > bins ? kLdsPerCu - bins : 0);
+  int S = env_int("TI_HX_STAGE", ilp);
+  S = std::max(1, std::min<int>(S, f->T));
+  while (S > 1 && S * stride > cap) --S;
+  if (S * stride > cap || S < std::min(ilp, f->T)) return false;
+  for (auto& rx : f->rx) pack_htop(d, slot_of, D0, &rx);
+  f->hx_top = D0;
+  f->hx_ilp = ilp;
+  f->hx_stage = S;
+  f->layout = 8;
+  return true;
+}
+
 // Mean depth of the leaves of a forest (every leaf counted once).
 double mean_leaf_depth(const ti_forest_desc* d) {
   double sum = 0;
@@ -1504,10 +1572,11 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
     if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
     d.leaves = lv;
     if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
-  } else if (f->layout == 6 || f->layout == 7) {
+  } else if (f->layout == 6 || f->layout == 7 || f->layout == 8) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.rx_recs[i], f->rx[i].recs, &d.bytes))) return rc;
       if ((rc = upload(&d.bx_tbl[i], f->rx[i].tbl, &d.bytes))) return rc;
+      if (f->layout == 8 && (rc = upload(&d.hx_top[i], f->rx[i].top, &d.bytes))) return rc;
     }
     if ((rc = upload(&d.rx_base, f->h_rx_base, &d.bytes))) return rc;
     if ((rc = upload(&d.rx_nint, f->h_rx_nint, &d.bytes))) return rc;
@@ -1600,6 +1669,13 @@ KernelFn select_lexplicit(int xdt, int accum, int K, bool z, int ilp) {
   return ti::kernels_df(7, K, true, z, true, ilp);
 }
 
+KernelFn select_hexplicit(int xdt, int accum, int K, bool z, int ilp) {
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(8, K, true, z, true, ilp);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(8, K, true, z, true, ilp);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(8, K, true, z, true, ilp);
+  return ti::kernels_df(8, K, true, z, true, ilp);
+}
+
 KernelFn select_sexplicit(int xdt, int accum, int K, bool b16, bool z, int ilp) {
   if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(5, K, true, z, b16, ilp);
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(5, K, true, z, b16, ilp);
@@ -1658,7 +1734,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     R = f->bh[xdt == TI_F64 ? 1 : 0].rows;
   } else if (f->layout == 4 || f->layout == 5) {
     R = f->bx[xdt == TI_F64 ? 1 : 0].rows;
-  } else if (f->layout == 6 || f->layout == 7) {
+  } else if (f->layout == 6 || f->layout == 7 || f->layout == 8) {
     R = f->rx[xdt == TI_F64 ? 1 : 0].rows;
   } else {
     R = 256;
@@ -1671,7 +1747,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   if (f->layout == 3) feat_bytes = static_cast<size_t>(f->bh[xdt == TI_F64 ? 1 : 0].words) * R * 4;
   if (f->layout == 4 || f->layout == 5)
     feat_bytes = static_cast<size_t>(f->bx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
-  if (f->layout == 6 || f->layout == 7)
+  if (f->layout == 6 || f->layout == 7 || f->layout == 8)
     feat_bytes = static_cast<size_t>(f->rx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
 
   KArgs a;
@@ -1835,6 +1911,35 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (lds > kLdsPerCu || static_cast<int64_t>(kLxPf) * 16 * R < f->lx_stage_cap)
       return fail(TI_ERR_UNSUPPORTED, "staged record layout exceeds LDS");
     KernelFn fn = select_lexplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp);
+    int rc = ensure_lds_attr(d.device, fn);
+    if (rc) return rc;
+    const int64_t grid = (rows + R - 1) / R;
+    if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    TI_HIP(hipGetLastError());
+    return TI_OK;
+  } else if (f->layout == 8) {
+    const int ii = xdt == TI_F64 ? 1 : 0;
+    const ti_forest::RecExplicit& rx = f->rx[ii];
+    a.rx_recs = d.rx_recs[ii];
+    a.rx_base = d.rx_base;
+    a.rx_nint = d.rx_nint;
+    a.leaf_base = d.leaf_base;
+    a.rx_slots = static_cast<uint32_t>(f->rx_slots);
+    a.leaves = d.leaves;
+    a.exp_leaf_ids = d.exp_leaf_ids;
+    a.bin_tbl = d.bx_tbl[ii];
+    a.bin_L = rx.L;
+    a.bin_words = rx.words;
+    a.trees = reinterpret_cast<const unsigned char*>(d.hx_top[ii]);
+    a.depth = f->hx_top;
+    a.tree_stride = static_cast<int64_t>(8) << f->hx_top;   // 2^(D0+1) u32
+    a.stage_trees = f->hx_stage;
+    a.stage_off = static_cast<int32_t>(align16(feat_bytes + 4));
+    lds = static_cast<size_t>(a.stage_off) + static_cast<size_t>(f->hx_stage) * a.tree_stride;
+    if (lds > kLdsPerCu || static_cast<int64_t>(kHxPf) * 16 * R < f->hx_stage * a.tree_stride)
+      return fail(TI_ERR_UNSUPPORTED, "heap-top layout exceeds LDS");
+    KernelFn fn = select_hexplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->hx_ilp);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -2515,7 +2620,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
   if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
   if (want == "explicit" || want == "bexplicit" || want == "sexplicit" || want == "rexplicit" ||
-      want == "lexplicit") {
+      want == "lexplicit" || want == "hexplicit") {
     use_heap = false;
     use_compact = false;
   }
@@ -2603,10 +2708,15 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         f->rx_ilp = md < 12.0 ? 16 : 8;
         const int force_ilp = env_int("TI_RX_ILP", 0);
         if (force_ilp > 0) f->rx_ilp = force_ilp >= 16 ? 16 : force_ilp >= 8 ? 8 : 4;
-        // small trees: staged in LDS (layout 7) unless layout 6 is forced
-        if (want != "rexplicit" && env_int("TI_NO_LEXPLICIT", 0) == 0 &&
-            plan_lx_stages(f.get(), f->T))
+        // small trees: staged in LDS (layout 7) unless layout 6 or 8 is forced;
+        // deep trees too large for a stage: heap tops in LDS (layout 8)
+        if (want != "rexplicit" && want != "hexplicit" && env_int("TI_NO_LEXPLICIT", 0) == 0 &&
+            plan_lx_stages(f.get(), f->T)) {
           f->layout = 7;
+        } else if (want == "hexplicit" ||
+                   (want != "rexplicit" && D >= kHxMinDepth && env_int("TI_NO_HEXPLICIT", 0) == 0)) {
+          plan_htop(desc, f.get(), slot_of, D);
+        }
       } else {
         for (auto& rx : f->rx) rx = ti_forest::RecExplicit();
         f->h_rx_base.clear();

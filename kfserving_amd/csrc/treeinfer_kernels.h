@@ -1331,8 +1331,13 @@ __device__ __forceinline__ uint16_t lds_u16(uint32_t byte_addr) {
 // (zero-missing forests) b2 = 2 b + (x == 0) and NaN = 0xFFFE.  Returns
 // (uniformly) whether the tile needs the slow step: a NaN, or with ZB an
 // exact 0.
+#ifndef TI_RX_POSTSTEP
+#define TI_RX_POSTSTEP 1   // layout 6: the group's loop test reads the lanes after the
+                           // step, so no pass runs once every lane is at its leaf
+#endif
 #ifndef TI_RX_BINQ
-#define TI_RX_BINQ 16   // features searched at once per lane (independent load chains)
+#define TI_RX_BINQ 8   // features searched at once per lane (independent load chains;
+                       // 16 measured slower on C3 and C4)
 #endif
 template <typename XT, bool ZB>
 __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
@@ -1430,6 +1435,62 @@ __device__ __forceinline__ void rx_leaves(const KArgs& a, ACC (&acc)[KMAX], int 
 
 typedef const __attribute__((address_space(4))) uint32_t rx_cu32;   // scalar-loaded tables
 
+// The lockstep descent of a group of ILP trees from each lane's current slot
+// (and the record gathered there) to its leaf.
+template <bool ZERO, bool SLOW, int ILP>
+__device__ __forceinline__ void rx_descend(const rx_rsrc_t rsrc, const uint32_t (&sb)[ILP],
+                                           const uint32_t (&ni)[ILP], uint32_t (&slot)[ILP],
+                                           rx_u2_t (&rec)[ILP], uint32_t lane_off) {
+#if TI_RX_POSTSTEP
+  bool in[ILP];
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < ILP; ++q) {
+    in[q] = slot[q] < ni[q];
+    any |= in[q];
+  }
+  while (__ballot(any) != 0) {   // a lane of the group is still inside a tree
+    uint32_t b[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q)   // a lane at its leaf reads its own column of word 0
+      b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
+    any = false;
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const uint32_t nx = rx_next<ZERO, SLOW>(rec[q].x, rec[q].y, (uint16_t)b[q]);
+      if (in[q]) {
+        slot[q] = nx;
+        rec[q] = rx_struct_load(rsrc, nx, 0u, sb[q], 0);
+      }
+      in[q] = slot[q] < ni[q];   // after the step: no pass once the last lane leaves
+      any |= in[q];
+    }
+  }
+#else
+  for (;;) {
+    bool in[ILP];
+    uint32_t b[ILP];
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      in[q] = slot[q] < ni[q];
+      any |= in[q];
+      // a lane at its leaf reads its own column of word 0 (conflict-free)
+      b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
+    }
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const uint32_t nx = rx_next<ZERO, SLOW>(rec[q].x, rec[q].y, (uint16_t)b[q]);
+      if (in[q]) {
+        slot[q] = nx;
+        rec[q] = rx_struct_load(rsrc, nx, 0u, sb[q], 0);
+      }
+    }
+    if (__ballot(any) == 0) break;   // every lane of every tree was at a leaf
+  }
+#endif
+}
+
 template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP>
 __device__ __forceinline__ void rx_walk(const KArgs& a, ACC (&acc)[KMAX], uint32_t lane_off,
                                         int64_t row, bool live) {
@@ -1449,27 +1510,7 @@ __device__ __forceinline__ void rx_walk(const KArgs& a, ACC (&acc)[KMAX], uint32
       slot[q] = 0u;
       rec[q] = rx_struct_load(rsrc, 0u, 0u, sb[q], 0);   // the root (or a lone leaf)
     }
-    for (;;) {
-      bool in[ILP];
-      uint32_t b[ILP];
-      bool any = false;
-#pragma unroll
-      for (int q = 0; q < ILP; ++q) {
-        in[q] = slot[q] < ni[q];
-        any |= in[q];
-        // a lane at its leaf reads its own column of word 0 (conflict-free)
-        b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
-      }
-#pragma unroll
-      for (int q = 0; q < ILP; ++q) {
-        const uint32_t nx = rx_next<ZERO, SLOW>(rec[q].x, rec[q].y, (uint16_t)b[q]);
-        if (in[q]) {
-          slot[q] = nx;
-          rec[q] = rx_struct_load(rsrc, nx, 0u, sb[q], 0);
-        }
-      }
-      if (__ballot(any) == 0) break;   // every lane of every tree was at a leaf
-    }
+    rx_descend<ZERO, SLOW, ILP>(rsrc, sb, ni, slot, rec, lane_off);
 #pragma unroll
     for (int q = 0; q < ILP; ++q)
       if (t0 + q < T)
@@ -1611,6 +1652,137 @@ __global__ void __launch_bounds__(512) lexplicit_predict_kernel(const KArgs a) {
     } else {
       if (vis) lx_stage<ACC, KMAX, ZERO, false, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
       else lx_stage<ACC, KMAX, ZERO, false, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+    }
+  }
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
+// ---- heap top + record bottom (layout 8) -----------------------------------
+// Deep forests whose trees are far larger than a stage (C4: sklearn depth 16,
+// ~7k nodes a tree) walk layout 6's gathers for every level, and those
+// gathers bound the kernel (TD busy ~0.9).  Layout 8 stages the top D0 levels
+// of each tree in LDS as a complete heap of layout 6's x words (1-based: node
+// i's children are 2i and 2i+1; below a shallow leaf, padding words that
+// always go left), followed at heap positions [2^D0, 2^(D0+1)) by the layout-6
+// slot where the walk continues (an internal node at depth D0, or the leaf
+// that ended the path above it).  A lane walks the top as the binned heap
+// kernel does -- the bin read and the read of the two children together, one
+// LDS round trip per level, every lane busy at every level -- and the rest of
+// the tree by layout 6's exec-masked gathers from that slot.  Leaves are
+// added in tree order, so sums are layout 6's, bit for bit.
+template <bool ZERO>
+__device__ __forceinline__ bool rx_right_slow(uint32_t x, uint32_t b) {
+  constexpr uint32_t kNan = ZERO ? 0xFFFEu : 0xFFFFu;
+  bool right = (x >> 16) < b;
+  if (ZERO) right = right != (((b & 1u) != 0u) && ((x & kRxZeroFlip) != 0u));
+  if (b == kNan) right = (x & kRxNanLeft) == 0u;
+  return right;
+}
+
+template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP>
+__device__ __forceinline__ void hx_stage(const KArgs& a, ACC (&acc)[KMAX], const rx_rsrc_t rsrc,
+                                         const unsigned char* stage, int t0, int cnt,
+                                         uint32_t lane_off, int64_t row, bool live) {
+  rx_cu32* rx_base = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* rx_nint = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_nint));
+  const int D0 = a.depth;
+  const int64_t stride = a.tree_stride;
+  for (int j = 0; j < cnt; j += ILP) {
+    const uint32_t* tp[ILP];
+    uint32_t idx[ILP], nd[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = (j + q) < cnt ? (j + q) : (cnt - 1);
+      tp[q] = reinterpret_cast<const uint32_t*>(stage + (int64_t)tq * stride);
+      idx[q] = 1u;
+      nd[q] = tp[q][1];   // the root: one broadcast read
+    }
+    for (int l = 0; l < D0; ++l) {   // the last level selects the bottom slot
+      uint32_t b[ILP];
+      uint2 pr[ILP];
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        b[q] = lds_u16((nd[q] & kRxOffMask) | lane_off);
+        pr[q] = *reinterpret_cast<const uint2*>(tp[q] + 2u * idx[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        if (!SLOW) {
+          // right = rank < bin, the child word from the pair, idx = 2 idx + right
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %2 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+              "v_cndmask_b32 %0, %3, %4, vcc\n\t"
+              "v_addc_co_u32 %1, vcc, %1, %1, vcc"
+              : "+v"(nd[q]), "+v"(idx[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y)
+              : "vcc");
+        } else {
+          const bool right = rx_right_slow<ZERO>(nd[q], b[q]);
+          idx[q] = idx[q] + idx[q] + (uint32_t)right;
+          nd[q] = right ? pr[q].y : pr[q].x;
+        }
+      }
+    }
+    uint32_t sb[ILP], ni[ILP], slot[ILP];
+    rx_u2_t rec[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = t0 + ((j + q) < cnt ? (j + q) : (cnt - 1));
+      sb[q] = rx_base[tq] << 3;
+      ni[q] = rx_nint[tq];
+      slot[q] = nd[q];
+      rec[q] = rx_struct_load(rsrc, slot[q], 0u, sb[q], 0);
+    }
+    rx_descend<ZERO, SLOW, ILP>(rsrc, sb, ni, slot, rec, lane_off);
+#pragma unroll
+    for (int q = 0; q < ILP; ++q)
+      if (j + q < cnt)
+        rx_leaves<ACC, KMAX>(a, acc, t0 + j + q, slot[q], ni[q], rec[q].x, rec[q].y, row, live,
+                             VIS);
+  }
+}
+
+// LDS: [bin image (bin_words * R u32)] [flag] ... [stage at stage_off: S tops]
+template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
+__global__ void __launch_bounds__(512) hexplicit_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int PF = 8;   // = kHxPf (host): a stage is at most PF x 16 B x R
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  unsigned char* stage = smem + a.stage_off;
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  const int T = a.n_trees;
+  const int S = a.stage_trees;
+  const int64_t stride = a.tree_stride;
+  const rx_rsrc_t rsrc = rx_make_rsrc(a.rx_recs, a.rx_slots);
+  u32x4 pf[PF];
+  prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees),
+                 (int)(((int64_t)(T < S ? T : S) * stride) >> 4), tid, R);
+  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid);
+  const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
+  ACC acc[KMAX];
+  init_acc(acc, a);
+  const int last0 = ((T - 1) / S) * S;
+  for (int t0 = 0; t0 < T; t0 += S) {
+    const int cnt = (T - t0) < S ? (T - t0) : S;
+    __syncthreads();   // the previous stage's walk is over
+    commit_n<PF>(pf, reinterpret_cast<u32x4*>(stage), (int)(((int64_t)cnt * stride) >> 4), tid, R);
+    __syncthreads();
+    {
+      const int tn = t0 + S <= last0 ? t0 + S : last0;
+      const int cn = (T - tn) < S ? (T - tn) : S;
+      prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees + (int64_t)tn * stride),
+                     (int)(((int64_t)cn * stride) >> 4), tid, R);
+    }
+    if (slow) {
+      if (vis) hx_stage<ACC, KMAX, ZERO, true, true, ILP>(a, acc, rsrc, stage, t0, cnt, lane_off, row, live);
+      else hx_stage<ACC, KMAX, ZERO, true, false, ILP>(a, acc, rsrc, stage, t0, cnt, lane_off, row, live);
+    } else {
+      if (vis) hx_stage<ACC, KMAX, ZERO, false, true, ILP>(a, acc, rsrc, stage, t0, cnt, lane_off, row, live);
+      else hx_stage<ACC, KMAX, ZERO, false, false, ILP>(a, acc, rsrc, stage, t0, cnt, lane_off, row, live);
     }
   }
   if (!live || a.kind == TI_OUTPUT_LEAF) return;

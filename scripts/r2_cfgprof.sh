@@ -19,5 +19,9 @@ prof() {  # out config settings
   run pmc_f --pmc FETCH_SIZE || return 1
   run pmc_w --pmc WRITE_SIZE || return 1
 }
-prof r2_c3_l7c c3 lexplicit:7 || exit 1
-prof r2_c4_l6c c4 rexplicit:8 || exit 1
+# usage: scripts/r2_cfgprof.sh [OUTNAME CONFIG SETTING]...  (default: C3 layout 7, C4 layout 8)
+if [ $# -eq 0 ]; then set -- r2_c3_l7c c3 lexplicit:7 r2_c4_l8 c4 hexplicit:8; fi
+while [ $# -ge 3 ]; do
+  prof "$1" "$2" "$3" || exit 1
+  shift 3
+done

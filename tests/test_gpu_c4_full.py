@@ -31,12 +31,16 @@ def _c4():
     return forest_from_sklearn(est), X, est.predict(X), est.apply(X), "fitted"
 
 
-def test_c4_full_model_bit_exact_vs_sklearn():
+@pytest.mark.parametrize("layout", [None, "rexplicit"])
+def test_c4_full_model_bit_exact_vs_sklearn(layout, monkeypatch):
+    """The default layout (8: heap tops in LDS, gathered bottoms) and layout 6."""
     f, X, want, leaves, src = _c4()
     assert f.n_trees == 200 and f.n_features == 64 and f.depths().max() == 16
     assert np.isnan(X).any() and X.shape[0] >= 4096
+    if layout:
+        monkeypatch.setenv("TI_FORCE_LAYOUT", layout)
     dev = DeviceForest(f, [0])
-    assert dev.info()["layout"] in (4, 6)
+    assert dev.info()["layout"] == (6 if layout else 8)
     assert np.array_equal(dev.predict(X, OUT_PREDICT), want), src
     assert np.array_equal(dev.predict(X, OUT_LEAF), leaves), src
     dev.close()

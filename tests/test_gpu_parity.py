@@ -341,11 +341,11 @@ def _dev_with_layout(forest, layout):
 
 
 LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2, "bheap": 3, "bexplicit": 4, "sexplicit": 5,
-             "rexplicit": 6, "lexplicit": 7}
+             "rexplicit": 6, "lexplicit": 7, "hexplicit": 8}
 
 
 @pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit", "rexplicit", "lexplicit"])
+                                    "sexplicit", "rexplicit", "lexplicit", "hexplicit"])
 def test_xgb_golden_every_layout(golden, layout):
     g = np.load(os.path.join(golden, "xgb_synth.npz"))
     trees, ti = xf.synthetic_complete_trees(40, 8, 28, seed=1)
@@ -361,7 +361,8 @@ def test_xgb_golden_every_layout(golden, layout):
     np.testing.assert_allclose(dev3.predict(g["X"], OUT_PREDICT), g["prob3"], rtol=RTOL)
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit", "lexplicit"])
+@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit",
+                                    "lexplicit", "hexplicit"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
     g = np.load(os.path.join(golden, "lgb_synth.npz"))
@@ -379,7 +380,7 @@ def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
 
 
 @pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit", "rexplicit", "lexplicit"])
+                                    "sexplicit", "rexplicit", "lexplicit", "hexplicit"])
 def test_lgb_iris_fixture_every_layout(golden, layout):
     from sklearn.datasets import load_iris
     path = os.path.join(golden, "lgb_iris_v3.txt")
@@ -389,7 +390,8 @@ def test_lgb_iris_fixture_every_layout(golden, layout):
     assert np.array_equal(dev.predict(X, OUT_MARGIN), lgb_ref.predict(m, X, raw_score=True))
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit", "lexplicit"])
+@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit",
+                                    "lexplicit", "hexplicit"])
 def test_sklearn_classifier_every_layout(golden, layout):
     fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
     gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
@@ -421,7 +423,7 @@ def test_compact_ragged_and_specials(rows):
                           port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
 
 
-@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit", "rexplicit", "lexplicit"])
+@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit", "rexplicit", "lexplicit", "hexplicit"])
 @pytest.mark.parametrize("rows", [1, 255, 257, 3000])
 def test_bexplicit_zero_missing_and_specials(rows, layout):
     """Binned explicit kernels (nodes in global memory / staged in LDS) on
@@ -446,10 +448,10 @@ def test_bexplicit_zero_missing_and_specials(rows, layout):
                           port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
 
 
-@pytest.mark.parametrize("layout", ["rexplicit", "lexplicit"])
+@pytest.mark.parametrize("layout", ["rexplicit", "lexplicit", "hexplicit"])
 @pytest.mark.parametrize("special", ["nan", "zero", "tiny", "none"])
 def test_record_layouts_fast_and_slow_tiles(layout, special):
-    """Layouts 6 / 7 walk tiles without NaN (and, for zero-missing forests,
+    """Layouts 6 / 7 / 8 walk tiles without NaN (and, for zero-missing forests,
     without exact zeros) with the 2-VALU rank step and the rest with the full
     rule: specials confined to a few rows put both kinds of tile in one batch,
     and every tile must agree with the C port bit for bit."""
@@ -477,6 +479,40 @@ def test_record_layouts_fast_and_slow_tiles(layout, special):
     dx = _dev_with_layout(xfo, layout)
     assert dx.info()["layout"] == LAYOUT_ID[layout]
     assert np.array_equal(dx.predict(X32, OUT_MARGIN), port.xgb_predict(xt, xti, 1, 0.0, 40, X32)[:, 0])
+
+
+@pytest.mark.parametrize("top", [1, 3, 6, 10])
+def test_heap_top_depths(top, monkeypatch):
+    """Layout 8 at several top depths: the heap top ends above, inside and
+    below the trees' leaves (leaf-wise trees of every missing type, padding
+    under shallow leaves, bottom slots that are leaves or internal nodes), the
+    stage holds one ILP group or several, and a tree ends in its top."""
+    monkeypatch.setenv("TI_HX_TOP", str(top))
+    monkeypatch.setenv("TI_HX_STAGE", "16" if top <= 6 else "4")
+    monkeypatch.setenv("TI_HX_ILP", "8" if top <= 6 else "4")
+    trees = lf.synthetic_leafwise_trees(37, 255, 40, seed=13)
+    trees.append(lf.synthetic_leafwise_trees(1, 2, 40, seed=14)[0])   # a 1-split tree
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, 40, "binary sigmoid:1")
+        f = load_lightgbm_model(p)
+    dev = _dev_with_layout(f, "hexplicit")
+    assert dev.info()["layout"] == 8
+    rng = np.random.default_rng(top)
+    X = rng.standard_normal((3001, 40))
+    sp = np.array([np.nan, 0.0, -0.0, 1e-40, np.inf, -np.inf])
+    mask = rng.random(X.shape) < 0.02
+    X[mask] = sp[rng.integers(0, len(sp), mask.sum())]
+    X[:1024][np.isnan(X[:1024])] = 0.5   # fast tiles first
+    X[:1024][X[:1024] == 0] = 0.5
+    want = port.lgb_predict_raw(trees, 1, 40, X)[:, 0]
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), want)
+    X32 = X.astype(np.float32)
+    assert np.array_equal(dev.predict(X32, OUT_MARGIN),
+                          port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
+    lm_leaf = dev.predict(X32, OUT_LEAF)
+    ref = _dev_with_layout(f, "rexplicit")
+    assert np.array_equal(lm_leaf, ref.predict(X32, OUT_LEAF))
 
 
 # ------------------------------------------------- sklearn GradientBoosting
