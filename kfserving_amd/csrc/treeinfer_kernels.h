@@ -700,7 +700,10 @@ __device__ __forceinline__ void bheap_stage(const KArgs& a, const unsigned char*
       idx[q] = 1u;
       nd[q] = tp[q][1];   // the root: one broadcast read
     }
-    for (int l = 0; l + 1 < D; ++l) {
+    // D levels: at the last one the children pair is two leaves (entries
+    // [2^D, 2^(D+1)) are the leaf slots), so with float leaves of width 1 the
+    // selected word is the leaf value itself -- no separate leaf read
+    for (int l = 0; l < D; ++l) {
       uint32_t b[kBTilp];
       uint2 pr[kBTilp];
 #pragma unroll
@@ -752,14 +755,6 @@ __device__ __forceinline__ void bheap_stage(const KArgs& a, const unsigned char*
         nd[q] = right ? pr[q].y : pr[q].x;
       }
     }
-    {   // last level: the children are leaves
-      uint32_t b[kBTilp];
-#pragma unroll
-      for (int q = 0; q < kBTilp; ++q) b[q] = lds_bin<B16>((nd[q] & kBNodeOffMask) | lane_off);
-#pragma unroll
-      for (int q = 0; q < kBTilp; ++q)
-        idx[q] = idx[q] + idx[q] + (uint32_t)!bin_left<B16, CHECK_NAN>(b[q], nd[q]);
-    }
 #pragma unroll
     for (int q = 0; q < kBTilp; ++q) {
       if (j + q < cnt) {
@@ -767,6 +762,9 @@ __device__ __forceinline__ void bheap_stage(const KArgs& a, const unsigned char*
         const int t = t0 + j + q;
         if (want_leaf) {
           if (live) static_cast<int32_t*>(a.out)[row * T + t] = a.heap_leaf_ids[(int64_t)t * NE + leaf];
+        } else if (sizeof(ACC) == 4 && a.leaf_width == 1) {
+          const ACC v = __uint_as_float(nd[q]);   // the leaf the last level selected
+          add_leaf<ACC, KMAX>(acc, &v, 0, 1, a.tree_group[t]);
         } else {
           const ACC* lv = reinterpret_cast<const ACC*>(tp[q] + NE);
           add_leaf<ACC, KMAX>(acc, lv, leaf, a.leaf_width, a.tree_group[t]);
