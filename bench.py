@@ -48,7 +48,7 @@ SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 4.0
 VALU_PEAK = SIMDS * CLOCK_HZ / VALU_CYCLES     # wave64 VALU instructions / s
 LAYOUT_NAMES = {0: "heap", 1: "explicit", 2: "compact", 3: "bheap", 4: "bexplicit",
                 5: "sexplicit", 6: "rexplicit", 7: "lexplicit",
-                8: "hexplicit"}
+                8: "hexplicit", 9: "texplicit"}
 
 
 def parse_args(argv=None):

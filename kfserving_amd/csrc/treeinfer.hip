@@ -527,6 +527,10 @@ struct ti_forest {
   // heap top + record bottom (layout 8): the top hx_top levels of each tree
   // staged in LDS hx_stage trees at a time, walked hx_ilp trees per lane
   int32_t hx_top = 0, hx_stage = 0, hx_ilp = 8;
+  // heap top + staged record bottom (layout 9): per tree [top | bottom] in
+  // rx[i].top, tree byte offsets [T+1] and bottom internal counts [T]; stages
+  // and ILP in h_lx_stage / lx_stage_cap / lx_ilp
+  std::vector<uint32_t> h_tx_off, h_tx_nint;
   std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
   // TreeSHAP (TI_OUTPUT_CONTRIB); has_shap = 0 when the forest has no covers.
   // The path tables are built and uploaded on the first contributions call
@@ -1398,6 +1402,126 @@ bool plan_htop(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t
   return true;
 }
 
+// Layout 9 (treeinfer_kernels.h, texplicit_predict_kernel): per tree, a heap
+// top of D0 levels (as layout 8's, the entries at [2^D0, 2^(D0+1)) holding
+// byte offsets into the bottom) and the bottom: layout 6's records from the
+// first internal node at depth >= D0 on (breadth-first order puts the top's
+// internal nodes first), children rebased to byte offsets from the bottom's
+// start, padded to 16 bytes.  Stages as layout 7's.  Returns false (the
+// caller keeps its choice) when two of the largest trees do not fit a stage
+// or a bottom exceeds 16-bit byte offsets.
+bool plan_tx(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>& slot_of, int D) {
+  int D0 = env_int("TI_TX_TOP", 6);
+  D0 = std::max(1, std::min(D0, std::min(D, 10)));
+  const int T = d->n_trees;
+  const size_t NE = size_t(1) << D0;
+  const uint32_t topb = static_cast<uint32_t>(8 * NE);
+  std::vector<int32_t> dep, q;
+  std::vector<uint32_t> ntop(T), nslots(T);
+  f->h_tx_off.assign(T + 1, 0);
+  f->h_tx_nint.assign(T, 0);
+  for (int t = 0; t < T; ++t) {
+    const int64_t b = d->tree_offset[t];
+    const int32_t n = static_cast<int32_t>(d->tree_offset[t + 1] - b);
+    dep.assign(n, 0);
+    q.assign(1, 0);
+    uint32_t nt = 0;
+    for (size_t qi = 0; qi < q.size(); ++qi) {
+      const int32_t v = q[qi];
+      const int64_t g = b + v;
+      if (d->feature[g] < 0) continue;
+      if (dep[v] < D0) ++nt;
+      dep[d->left[g]] = dep[d->right[g]] = dep[v] + 1;
+      q.push_back(d->left[g]);
+      q.push_back(d->right[g]);
+    }
+    ntop[t] = nt;
+    nslots[t] = static_cast<uint32_t>(n) - nt;
+    if (static_cast<size_t>(nslots[t]) * 8 > 65528) {
+      f->h_tx_off.clear();
+      f->h_tx_nint.clear();
+      return false;
+    }
+    f->h_tx_nint[t] = f->h_rx_nint[t] - nt;
+    const uint64_t end = f->h_tx_off[t] + topb + ((static_cast<uint64_t>(nslots[t]) * 8 + 15) & ~uint64_t(15));
+    if (end > 0xFFFFFFF0ull) {
+      f->h_tx_off.clear();
+      f->h_tx_nint.clear();
+      return false;
+    }
+    f->h_tx_off[t + 1] = static_cast<uint32_t>(end);
+  }
+  // stages: as plan_lx_stages
+  const int R = f->rx[0].rows;
+  if (f->rx[1].rows != R) return false;
+  const size_t bins = align16(static_cast<size_t>(std::max(f->rx[0].words, f->rx[1].words)) * R * 4 + 4);
+  const int wgs = std::max(1, env_int("TI_LX_WGS", 2));
+  size_t cap = kLdsPerCu / static_cast<size_t>(wgs);
+  cap = cap > bins ? cap - bins : 0;
+  cap = std::min(cap, static_cast<size_t>(kLxPf) * 16 * R) & ~size_t(15);
+  const std::vector<uint32_t>& o = f->h_tx_off;
+  size_t biggest = 0;
+  for (int t = 0; t < T; ++t) biggest = std::max<size_t>(biggest, o[t + 1] - o[t]);
+  if (T < 2 || cap < 2 * biggest) {
+    f->h_tx_off.clear();
+    f->h_tx_nint.clear();
+    return false;
+  }
+  std::vector<int32_t> stages(1, 0);
+  int t0 = 0;
+  while (t0 < T) {
+    int t1 = t0 + 1;
+    while (t1 < T && o[t1 + 1] - o[t0] <= cap) ++t1;
+    stages.push_back(t1);
+    t0 = t1;
+  }
+  // images: one per input view (the x words carry that view's ranks)
+  for (auto& rx : f->rx) {
+    rx.top.assign(o[T] / 4, 0u);
+    struct Item { int32_t v; uint32_t p; int l; };
+    std::vector<Item> st;
+    for (int t = 0; t < T; ++t) {
+      const int64_t b = d->tree_offset[t];
+      const uint32_t nt = ntop[t];
+      uint32_t* top = &rx.top[o[t] / 4];
+      uint2* bot = reinterpret_cast<uint2*>(top + 2 * NE);
+      st.assign(1, Item{0, 1u, 0});
+      while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        const int64_t g = b + it.v;
+        if (it.l == D0) {
+          top[it.p] = (slot_of[g] - nt) * 8u;
+          continue;
+        }
+        const bool leaf = d->feature[g] < 0;
+        top[it.p] = leaf ? kHxPad : rx.recs[b + slot_of[g]].x;
+        st.push_back(Item{leaf ? it.v : d->left[g], 2 * it.p, it.l + 1});
+        st.push_back(Item{leaf ? it.v : d->right[g], 2 * it.p + 1, it.l + 1});
+      }
+      // a leaf that ends a path above depth D0 is entered through the top:
+      // its bottom entries were set by the walk above (slot_of - nt)
+      for (uint32_t v = nt; v < nt + nslots[t]; ++v) {
+        uint2 r = rx.recs[b + v];
+        if (v < f->h_rx_nint[t]) {
+          const uint32_t lft = (r.y & 0xFFFFu) - nt, rgt = (r.y >> 16) - nt;
+          r.y = ((rgt * 8u) << 16) | (lft * 8u);
+        }
+        bot[v - nt] = r;
+      }
+    }
+  }
+  f->h_lx_stage = stages;
+  f->lx_stage_cap = static_cast<int64_t>(cap);
+  const double per_stage = static_cast<double>(T) / static_cast<double>(stages.size() - 1);
+  f->lx_ilp = per_stage >= 7.5 ? 8 : per_stage >= 6.5 ? 7 : 4;
+  const int force_ilp = env_int("TI_LX_ILP", 0);
+  if (force_ilp > 0) f->lx_ilp = force_ilp >= 8 ? 8 : force_ilp == 7 ? 7 : 4;
+  f->hx_top = D0;
+  f->layout = 9;
+  return true;
+}
+
 // Mean depth of the leaves of a forest (every leaf counted once).
 double mean_leaf_depth(const ti_forest_desc* d) {
   double sum = 0;
@@ -1588,6 +1712,21 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
       d.leaves = lv;
     }
     if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
+  } else if (f->layout == 9) {
+    for (int i = 0; i < 2; ++i) {
+      if ((rc = upload(&d.hx_top[i], f->rx[i].top, &d.bytes))) return rc;
+      if ((rc = upload(&d.bx_tbl[i], f->rx[i].tbl, &d.bytes))) return rc;
+    }
+    if ((rc = upload(&d.rx_base, f->h_tx_off, &d.bytes))) return rc;
+    if ((rc = upload(&d.rx_nint, f->h_tx_nint, &d.bytes))) return rc;
+    if ((rc = upload(&d.lx_stage, f->h_lx_stage, &d.bytes))) return rc;
+    if ((rc = upload(&d.leaf_base, f->h_leaf_base, &d.bytes))) return rc;
+    if (f->LW > 1) {   // vector leaves are read from the leaf table
+      unsigned char* lv = nullptr;
+      if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
+      d.leaves = lv;
+    }
+    if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
   } else if (f->layout == 5) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.bh_img[i], f->bx[i].sx, &d.bytes))) return rc;
@@ -1669,6 +1808,13 @@ KernelFn select_lexplicit(int xdt, int accum, int K, bool z, int ilp) {
   return ti::kernels_df(7, K, true, z, true, ilp);
 }
 
+KernelFn select_texplicit(int xdt, int accum, int K, bool z, int ilp) {
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(9, K, true, z, true, ilp);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(9, K, true, z, true, ilp);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(9, K, true, z, true, ilp);
+  return ti::kernels_df(9, K, true, z, true, ilp);
+}
+
 KernelFn select_hexplicit(int xdt, int accum, int K, bool z, int ilp) {
   if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(8, K, true, z, true, ilp);
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(8, K, true, z, true, ilp);
@@ -1734,7 +1880,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     R = f->bh[xdt == TI_F64 ? 1 : 0].rows;
   } else if (f->layout == 4 || f->layout == 5) {
     R = f->bx[xdt == TI_F64 ? 1 : 0].rows;
-  } else if (f->layout == 6 || f->layout == 7 || f->layout == 8) {
+  } else if (f->layout >= 6 && f->layout <= 9) {
     R = f->rx[xdt == TI_F64 ? 1 : 0].rows;
   } else {
     R = 256;
@@ -1747,7 +1893,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   if (f->layout == 3) feat_bytes = static_cast<size_t>(f->bh[xdt == TI_F64 ? 1 : 0].words) * R * 4;
   if (f->layout == 4 || f->layout == 5)
     feat_bytes = static_cast<size_t>(f->bx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
-  if (f->layout == 6 || f->layout == 7 || f->layout == 8)
+  if (f->layout >= 6 && f->layout <= 9)
     feat_bytes = static_cast<size_t>(f->rx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
 
   KArgs a;
@@ -1911,6 +2057,33 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (lds > kLdsPerCu || static_cast<int64_t>(kLxPf) * 16 * R < f->lx_stage_cap)
       return fail(TI_ERR_UNSUPPORTED, "staged record layout exceeds LDS");
     KernelFn fn = select_lexplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp);
+    int rc = ensure_lds_attr(d.device, fn);
+    if (rc) return rc;
+    const int64_t grid = (rows + R - 1) / R;
+    if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    TI_HIP(hipGetLastError());
+    return TI_OK;
+  } else if (f->layout == 9) {
+    const int ii = xdt == TI_F64 ? 1 : 0;
+    const ti_forest::RecExplicit& rx = f->rx[ii];
+    a.trees = reinterpret_cast<const unsigned char*>(d.hx_top[ii]);
+    a.depth = f->hx_top;
+    a.rx_base = d.rx_base;   // tree byte offsets in the image
+    a.rx_nint = d.rx_nint;   // bottom internal nodes
+    a.leaf_base = d.leaf_base;
+    a.leaves = d.leaves;
+    a.exp_leaf_ids = d.exp_leaf_ids;
+    a.bin_tbl = d.bx_tbl[ii];
+    a.bin_L = rx.L;
+    a.bin_words = rx.words;
+    a.stage_start = d.lx_stage;
+    a.n_stages = static_cast<int32_t>(f->h_lx_stage.size() - 1);
+    a.stage_off = static_cast<int32_t>(align16(feat_bytes + 4));
+    lds = std::max(static_cast<size_t>(a.stage_off) + static_cast<size_t>(f->lx_stage_cap), kLxMinLds);
+    if (lds > kLdsPerCu || static_cast<int64_t>(kLxPf) * 16 * R < f->lx_stage_cap)
+      return fail(TI_ERR_UNSUPPORTED, "heap-top staged layout exceeds LDS");
+    KernelFn fn = select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -2620,7 +2793,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
   if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
   if (want == "explicit" || want == "bexplicit" || want == "sexplicit" || want == "rexplicit" ||
-      want == "lexplicit" || want == "hexplicit") {
+      want == "lexplicit" || want == "hexplicit" || want == "texplicit") {
     use_heap = false;
     use_compact = false;
   }
@@ -2708,10 +2881,16 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         f->rx_ilp = md < 12.0 ? 16 : 8;
         const int force_ilp = env_int("TI_RX_ILP", 0);
         if (force_ilp > 0) f->rx_ilp = force_ilp >= 16 ? 16 : force_ilp >= 8 ? 8 : 4;
-        // small trees: staged in LDS (layout 7) unless layout 6 or 8 is forced;
-        // deep trees too large for a stage: heap tops in LDS (layout 8)
-        if (want != "rexplicit" && want != "hexplicit" && env_int("TI_NO_LEXPLICIT", 0) == 0 &&
-            plan_lx_stages(f.get(), f->T)) {
+        // small trees: a heap top and the rest staged in LDS (layout 9; C3
+        // 1M rows 5.83 vs 6.15 ms for layout 7), or all records staged
+        // (layout 7, forced or TI_NO_TEXPLICIT=1); deep trees too large for a
+        // stage: heap tops in LDS, the rest gathered (layout 8)
+        const bool auto_ok = want != "rexplicit" && want != "hexplicit" && want != "lexplicit";
+        if ((want == "texplicit" || (auto_ok && env_int("TI_NO_TEXPLICIT", 0) == 0)) &&
+            plan_tx(desc, f.get(), slot_of, D)) {
+          // layout 9
+        } else if ((want == "lexplicit" || auto_ok) && env_int("TI_NO_LEXPLICIT", 0) == 0 &&
+                   plan_lx_stages(f.get(), f->T)) {
           f->layout = 7;
         } else if (want == "hexplicit" ||
                    (want != "rexplicit" && D >= kHxMinDepth && env_int("TI_NO_HEXPLICIT", 0) == 0)) {

@@ -11,12 +11,22 @@ using KernelFn = void (*)(KArgs);
 
 // layout: 0 heap, 1 explicit, 2 compact, 3 binned heap, 4 binned explicit,
 // 5 staged binned explicit, 6 record explicit, 7 staged record explicit,
-// 8 heap top + record bottom.
+// 8 heap top + record bottom, 9 heap top + staged record bottom.
 // fl: feature image in
 // LDS; z: LightGBM zero rule; b16 / pf: binned heap bin width and prefetch
 // depth.
 template <typename XT, typename ACC, int KMAX>
 KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
+  if (layout == 9) {   // pf carries the tree ILP (4, 7 or 8)
+    if constexpr (sizeof(ACC) == 8) {
+      if (z) return pf >= 8 ? texplicit_predict_kernel<XT, ACC, KMAX, true, 8>
+                    : pf == 7 ? texplicit_predict_kernel<XT, ACC, KMAX, true, 7>
+                              : texplicit_predict_kernel<XT, ACC, KMAX, true, 4>;
+    }
+    return pf >= 8 ? texplicit_predict_kernel<XT, ACC, KMAX, false, 8>
+           : pf == 7 ? texplicit_predict_kernel<XT, ACC, KMAX, false, 7>
+                     : texplicit_predict_kernel<XT, ACC, KMAX, false, 4>;
+  }
   if (layout == 8) {   // pf carries the tree ILP (4 or 8)
     if constexpr (sizeof(ACC) == 8) {
       if (z) return pf >= 8 ? hexplicit_predict_kernel<XT, ACC, KMAX, true, 8>

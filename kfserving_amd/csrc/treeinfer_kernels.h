@@ -1787,4 +1787,136 @@ __global__ void __launch_bounds__(512) hexplicit_predict_kernel(const KArgs a) {
   finish_row<ACC, KMAX>(acc, a, row);
 }
 
+// ---- heap top + staged bottom (layout 9) -----------------------------------
+// Layout 7 with the top D0 levels of each tree as a binned heap.  Per tree the
+// image holds [top: 2^(D0+1) u32 as layout 8's, except that the entries at
+// [2^D0, 2^(D0+1)) are byte offsets into the bottom] [bottom: layout 7's
+// records of the nodes at depth >= D0 and of every leaf, children as byte
+// offsets from the bottom's start], padded to 16 bytes; stages are runs of
+// consecutive trees, copied as layout 7 copies them.  A lane walks the top D0
+// levels with one LDS round trip and 3 VALU a level and no lane idle (the
+// lockstep of layout 7 costs two round trips and 8 VALU a step, and its
+// group runs for its deepest path), then the bottom in layout 7's lockstep.
+// KArgs: trees = image, depth = D0, rx_base = byte offset of each tree in the
+// image [T+1], rx_nint = internal nodes of each bottom [T].
+template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP>
+__device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t0, int t1,
+                                         uint32_t sbase, uint32_t lane_off, int64_t row,
+                                         bool live) {
+  rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* tx_nint = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_nint));
+  const int D0 = a.depth;
+  const uint32_t topb = 8u << D0;   // 2^(D0+1) u32
+  for (int j = t0; j < t1; j += ILP) {
+    uint32_t base[ILP], ni8[ILP], at[ILP], idx[ILP], nd[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = (j + q) < t1 ? (j + q) : (t1 - 1);
+      base[q] = sbase + tx_off[tq];
+      ni8[q] = tx_nint[tq] << 3;
+      idx[q] = 1u;
+      nd[q] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+          static_cast<uintptr_t>(base[q] + 4u));   // the root: one broadcast read
+    }
+    for (int l = 0; l < D0; ++l) {   // the last level selects the bottom entry
+      uint32_t b[ILP];
+      rx_u2_t pr[ILP];
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        b[q] = lds_u16((nd[q] & kRxOffMask) | lane_off);
+        pr[q] = lx_rec(base[q] + 8u * idx[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        if (!SLOW) {
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %2 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+              "v_cndmask_b32 %0, %3, %4, vcc\n\t"
+              "v_addc_co_u32 %1, vcc, %1, %1, vcc"
+              : "+v"(nd[q]), "+v"(idx[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y)
+              : "vcc");
+        } else {
+          const bool right = rx_right_slow<ZERO>(nd[q], b[q]);
+          idx[q] = idx[q] + idx[q] + (uint32_t)right;
+          nd[q] = right ? pr[q].y : pr[q].x;
+        }
+      }
+    }
+    rx_u2_t rec[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      base[q] += topb;   // the bottom
+      at[q] = nd[q];
+      rec[q] = lx_rec(base[q] + at[q]);
+    }
+    for (;;) {
+      bool in[ILP];
+      uint32_t b[ILP];
+      bool any = false;
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        in[q] = at[q] < ni8[q];
+        any |= in[q];
+        b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
+      }
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        const uint32_t nx = rx_next<ZERO, SLOW>(rec[q].x, rec[q].y, (uint16_t)b[q]);
+        at[q] = in[q] ? nx : at[q];
+        rec[q] = lx_rec(base[q] + at[q]);
+      }
+      if (__ballot(any) == 0) break;
+    }
+#pragma unroll
+    for (int q = 0; q < ILP; ++q)
+      if (j + q < t1)
+        rx_leaves<ACC, KMAX>(a, acc, j + q, at[q] >> 3, ni8[q] >> 3, rec[q].x, rec[q].y, row, live,
+                             VIS);
+  }
+}
+
+template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
+__global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int PF = 8;   // = kLxPf (host): a stage is at most PF x 16 B x R
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  u32x4* stage = reinterpret_cast<u32x4*>(smem + a.stage_off);
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* sst = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.stage_start));
+  const unsigned char* img = a.trees;
+  const int NS = a.n_stages;
+  auto lo_of = [&](int s) { return tx_off[sst[s]]; };   // trees start 16-byte aligned
+  auto n16_of = [&](int s) { return (int)((tx_off[sst[s + 1]] - tx_off[sst[s]]) >> 4); };
+  u32x4 pf[PF];
+  prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(0)), n16_of(0), tid, R);
+  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid);
+  const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
+  ACC acc[KMAX];
+  init_acc(acc, a);
+  for (int s = 0; s < NS; ++s) {
+    const int t0 = (int)sst[s], t1 = (int)sst[s + 1];
+    const uint32_t lo = lo_of(s);
+    __syncthreads();   // the previous stage's walk is over
+    commit_n<PF>(pf, stage, n16_of(s), tid, R);
+    __syncthreads();
+    const int sn = s + 1 < NS ? s + 1 : s;
+    prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(sn)), n16_of(sn), tid, R);
+    const uint32_t sbase = (uint32_t)a.stage_off - lo;   // LDS address = sbase + image byte
+    if (slow) {
+      if (vis) tx_stage<ACC, KMAX, ZERO, true, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+      else tx_stage<ACC, KMAX, ZERO, true, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+    } else {
+      if (vis) tx_stage<ACC, KMAX, ZERO, false, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+      else tx_stage<ACC, KMAX, ZERO, false, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+    }
+  }
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
 }  // namespace ti

@@ -19,9 +19,9 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 
-def c3_forest():
+def c3_forest(n_trees=1000):
     from kfserving_amd.formats import lightgbm_format as lf
-    trees = lf.synthetic_leafwise_trees(1000, 255, 100, seed=1)
+    trees = lf.synthetic_leafwise_trees(1000, 255, 100, seed=1)[:n_trees]
     with tempfile.TemporaryDirectory() as d:
         p = os.path.join(d, "model.txt")
         lf.write_lightgbm_text(p, trees, 100, "binary sigmoid:1")
@@ -40,6 +40,7 @@ def main():
     p.add_argument("--rows", type=int, default=1_000_000)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--nan", type=float, default=0.0)
+    p.add_argument("--trees", type=int, default=0, help="C3: the first N trees only (0 = all)")
     p.add_argument("--settings", default="rexplicit:16,lexplicit:8,lexplicit:4,rexplicit:8")
     a = p.parse_args()
     import torch
@@ -47,7 +48,8 @@ def main():
     from kfserving_amd.engine import DeviceForest
     from kfserving_amd.forest import OUT_MARGIN, TI_F32
     for c in a.configs.split(","):
-        f, F = {"c3": c3_forest, "c4": c4_forest}[c]()
+        f, F = (c3_forest(a.trees) if c == "c3" and a.trees else
+                {"c3": c3_forest, "c4": c4_forest}[c]())
         X = device_normal(a.rows, F, seed=3)
         if a.nan > 0:
             g = torch.Generator(device="cuda")
@@ -70,7 +72,8 @@ def main():
             if ref is None:
                 ref = o
             print(json.dumps({"config": c, "layout": lay, "got_layout": dev.info()["layout"],
-                              "ilp": int(ilp), "env": extra, "rows": a.rows, "nan": a.nan, "kernel_ms": kms,
+                              "ilp": int(ilp), "env": extra, "rows": a.rows, "nan": a.nan,
+                              "trees": a.trees or None, "kernel_ms": kms,
                               "rows_per_s": a.rows / (kms * 1e-3),
                               "same_as_first": bool(np.array_equal(o, ref))}), flush=True)
             dev.close()

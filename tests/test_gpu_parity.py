@@ -341,11 +341,13 @@ def _dev_with_layout(forest, layout):
 
 
 LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2, "bheap": 3, "bexplicit": 4, "sexplicit": 5,
-             "rexplicit": 6, "lexplicit": 7, "hexplicit": 8}
+             "rexplicit": 6, "lexplicit": 7, "hexplicit": 8,
+             "texplicit": 9}
 
 
 @pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit", "rexplicit", "lexplicit", "hexplicit"])
+                                    "sexplicit", "rexplicit", "lexplicit", "hexplicit",
+                                    "texplicit"])
 def test_xgb_golden_every_layout(golden, layout):
     g = np.load(os.path.join(golden, "xgb_synth.npz"))
     trees, ti = xf.synthetic_complete_trees(40, 8, 28, seed=1)
@@ -362,7 +364,7 @@ def test_xgb_golden_every_layout(golden, layout):
 
 
 @pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit",
-                                    "lexplicit", "hexplicit"])
+                                    "lexplicit", "hexplicit", "texplicit"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
     g = np.load(os.path.join(golden, "lgb_synth.npz"))
@@ -380,7 +382,8 @@ def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
 
 
 @pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit", "rexplicit", "lexplicit", "hexplicit"])
+                                    "sexplicit", "rexplicit", "lexplicit", "hexplicit",
+                                    "texplicit"])
 def test_lgb_iris_fixture_every_layout(golden, layout):
     from sklearn.datasets import load_iris
     path = os.path.join(golden, "lgb_iris_v3.txt")
@@ -391,7 +394,7 @@ def test_lgb_iris_fixture_every_layout(golden, layout):
 
 
 @pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit",
-                                    "lexplicit", "hexplicit"])
+                                    "lexplicit", "hexplicit", "texplicit"])
 def test_sklearn_classifier_every_layout(golden, layout):
     fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
     gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
@@ -423,7 +426,8 @@ def test_compact_ragged_and_specials(rows):
                           port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
 
 
-@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit", "rexplicit", "lexplicit", "hexplicit"])
+@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit", "rexplicit", "lexplicit", "hexplicit",
+                                    "texplicit"])
 @pytest.mark.parametrize("rows", [1, 255, 257, 3000])
 def test_bexplicit_zero_missing_and_specials(rows, layout):
     """Binned explicit kernels (nodes in global memory / staged in LDS) on
@@ -448,10 +452,10 @@ def test_bexplicit_zero_missing_and_specials(rows, layout):
                           port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
 
 
-@pytest.mark.parametrize("layout", ["rexplicit", "lexplicit", "hexplicit"])
+@pytest.mark.parametrize("layout", ["rexplicit", "lexplicit", "hexplicit", "texplicit"])
 @pytest.mark.parametrize("special", ["nan", "zero", "tiny", "none"])
 def test_record_layouts_fast_and_slow_tiles(layout, special):
-    """Layouts 6 / 7 / 8 walk tiles without NaN (and, for zero-missing forests,
+    """Layouts 6 to 9 walk tiles without NaN (and, for zero-missing forests,
     without exact zeros) with the 2-VALU rank step and the rest with the full
     rule: specials confined to a few rows put both kinds of tile in one batch,
     and every tile must agree with the C port bit for bit."""
@@ -481,13 +485,16 @@ def test_record_layouts_fast_and_slow_tiles(layout, special):
     assert np.array_equal(dx.predict(X32, OUT_MARGIN), port.xgb_predict(xt, xti, 1, 0.0, 40, X32)[:, 0])
 
 
-@pytest.mark.parametrize("top", [1, 3, 6, 10])
-def test_heap_top_depths(top, monkeypatch):
-    """Layout 8 at several top depths: the heap top ends above, inside and
-    below the trees' leaves (leaf-wise trees of every missing type, padding
-    under shallow leaves, bottom slots that are leaves or internal nodes), the
-    stage holds one ILP group or several, and a tree ends in its top."""
+@pytest.mark.parametrize("layout,top", [("hexplicit", 1), ("hexplicit", 3), ("hexplicit", 6),
+                                        ("hexplicit", 10), ("texplicit", 1), ("texplicit", 4),
+                                        ("texplicit", 6), ("texplicit", 9)])
+def test_heap_top_depths(layout, top, monkeypatch):
+    """Layouts 8 and 9 at several top depths: the heap top ends above, inside
+    and below the trees' leaves (leaf-wise trees of every missing type, padding
+    under shallow leaves, bottom entries that are leaves or internal nodes),
+    the stage holds one ILP group or several, and a tree ends in its top."""
     monkeypatch.setenv("TI_HX_TOP", str(top))
+    monkeypatch.setenv("TI_TX_TOP", str(top))
     monkeypatch.setenv("TI_HX_STAGE", "16" if top <= 6 else "4")
     monkeypatch.setenv("TI_HX_ILP", "8" if top <= 6 else "4")
     trees = lf.synthetic_leafwise_trees(37, 255, 40, seed=13)
@@ -496,8 +503,8 @@ def test_heap_top_depths(top, monkeypatch):
         p = os.path.join(d, "model.txt")
         lf.write_lightgbm_text(p, trees, 40, "binary sigmoid:1")
         f = load_lightgbm_model(p)
-    dev = _dev_with_layout(f, "hexplicit")
-    assert dev.info()["layout"] == 8
+    dev = _dev_with_layout(f, layout)
+    assert dev.info()["layout"] == LAYOUT_ID[layout]
     rng = np.random.default_rng(top)
     X = rng.standard_normal((3001, 40))
     sp = np.array([np.nan, 0.0, -0.0, 1e-40, np.inf, -np.inf])
