@@ -151,7 +151,11 @@ typedef struct ti_forest ti_forest;   /* opaque, owns device memory */
 
 /* Layout the engine chose for a forest (diagnostics, bench byte models). */
 typedef struct ti_forest_info {
-  int32_t layout;             /* 0 = heap (complete, LDS-staged), 1 = explicit nodes */
+  int32_t layout;             /* 0 heap (complete, LDS-staged), 1 explicit nodes,
+                                 2 compact, 3 binned heap, 4 binned explicit, 5 staged
+                                 binned explicit, 6 record explicit (gathered), 7 staged
+                                 records, 8 heap tops + gathered records, 9 heap tops +
+                                 staged records               */
   int32_t depth;              /* heap depth D, or max depth for explicit             */
   int32_t n_trees;
   int32_t n_groups;
