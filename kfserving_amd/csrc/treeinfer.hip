@@ -514,6 +514,7 @@ struct ti_forest {
     int32_t L = 0;
     int32_t rows = 256;
     int32_t words = 0;
+    int32_t kary = 0;            // > 0: tbl holds 5-ary search tables of this height
     std::vector<uint32_t> top;   // heap tops (layout 8): [T][2^(hx_top+1)] u32
   } rx[2];
   std::vector<uint32_t> h_rx_base, h_rx_nint;   // h_rx_base: [T+1]
@@ -1023,6 +1024,43 @@ void eytzinger_tables(const RankTables<XT>& rt, std::vector<unsigned char>* out)
   }
 }
 
+// 5-ary search tables (float32 view of layouts 6-9, rx_stage_bins): per
+// feature a complete 5-ary tree of height H, node j (0-based, children
+// 5j+1 .. 5j+5) holding 4 keys, filled in order with the sorted thresholds and
+// +inf padding.  The search counts the keys below x at each node and descends;
+// after H levels, j - (5^H - 1)/4 = #{u < x}: the same rank as the Eytzinger
+// search, in H 16-byte gathers instead of L 4-byte ones.
+void kary_fill(const std::vector<float>& srt, std::vector<float>* out, size_t j, int level, int H,
+               size_t* i) {
+  if (level == H) return;
+  for (int c = 0; c < 4; ++c) {
+    kary_fill(srt, out, 5 * j + 1 + c, level + 1, H, i);
+    (*out)[4 * j + c] = *i < srt.size() ? srt[*i] : INFINITY;
+    ++*i;
+  }
+  kary_fill(srt, out, 5 * j + 5, level + 1, H, i);
+}
+
+void kary_tables(const RankTables<float>& rt, std::vector<unsigned char>* out, int* height) {
+  const int F = static_cast<int>(rt.u.size());
+  int H = 1;
+  size_t p5 = 5;
+  while (p5 - 1 < rt.m_max) {
+    p5 *= 5;
+    ++H;
+  }
+  const size_t nn = (p5 - 1) / 4;
+  out->assign(static_cast<size_t>(F) * nn * 16, 0);
+  std::vector<float> node(nn * 4), srt;
+  for (int f = 0; f < F; ++f) {
+    srt.assign(rt.u[f].begin(), rt.u[f].end());
+    size_t i = 0;
+    kary_fill(srt, &node, 0, 0, H, &i);
+    std::memcpy(out->data() + static_cast<size_t>(f) * nn * 16, node.data(), nn * 16);
+  }
+  *height = H;
+}
+
 template <typename XT, typename ACC>
 bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
                 std::vector<int32_t>* leaf_ids) {
@@ -1255,7 +1293,13 @@ bool pack_rexplicit(const ti_forest_desc* d, const ti_forest* f,
   if (static_cast<size_t>(rx->words) * R * 4 > kFeatLdsMax) return false;
   rx->rows = R;
   rx->L = rt.L;
-  eytzinger_tables(rt, &rx->tbl);
+  rx->kary = 0;
+  if constexpr (sizeof(XT) == 4) {
+    if (env_int("TI_KARY", 1) != 0) kary_tables(rt, &rx->tbl, &rx->kary);
+    else eytzinger_tables(rt, &rx->tbl);
+  } else {
+    eytzinger_tables(rt, &rx->tbl);
+  }
   // an even slot count: the staged layout copies whole 16-byte words
   rx->recs.assign(d->n_nodes + (d->n_nodes & 1), uint2{0u, 0u});
   const bool scalar_leaves = d->leaf_width == 1;
@@ -2027,6 +2071,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.exp_leaf_ids = d.exp_leaf_ids;
     a.bin_tbl = d.bx_tbl[ii];
     a.bin_L = rx.L;
+    a.bin_kary = rx.kary;
     a.bin_words = rx.words;
     lds = feat_bytes + 16;
     KernelFn fn = select_rexplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->rx_ilp);
@@ -2049,6 +2094,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.exp_leaf_ids = d.exp_leaf_ids;
     a.bin_tbl = d.bx_tbl[ii];
     a.bin_L = rx.L;
+    a.bin_kary = rx.kary;
     a.bin_words = rx.words;
     a.stage_start = d.lx_stage;
     a.n_stages = static_cast<int32_t>(f->h_lx_stage.size() - 1);
@@ -2076,6 +2122,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.exp_leaf_ids = d.exp_leaf_ids;
     a.bin_tbl = d.bx_tbl[ii];
     a.bin_L = rx.L;
+    a.bin_kary = rx.kary;
     a.bin_words = rx.words;
     a.stage_start = d.lx_stage;
     a.n_stages = static_cast<int32_t>(f->h_lx_stage.size() - 1);
@@ -2103,6 +2150,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.exp_leaf_ids = d.exp_leaf_ids;
     a.bin_tbl = d.bx_tbl[ii];
     a.bin_L = rx.L;
+    a.bin_kary = rx.kary;
     a.bin_words = rx.words;
     a.trees = reinterpret_cast<const unsigned char*>(d.hx_top[ii]);
     a.depth = f->hx_top;

@@ -117,6 +117,7 @@ struct KArgs {
   // binned layouts: rank images of the features (see stage_bins)
   const void* bin_tbl;            // [F][2^bin_L] Eytzinger threshold tables, XT
   int32_t bin_L;                  // search depth (common to all features)
+  int32_t bin_kary;               // > 0: float32 5-ary search tables of this height (rx_stage_bins)
   int32_t bin_words;              // packed bin words per row (C)
   int32_t bin_chunk;              // columns binned per pass through the temp area
   int32_t stage_off;              // LDS byte offset of the tree stage / temp area
@@ -1337,9 +1338,15 @@ __device__ __forceinline__ uint16_t lds_u16(uint32_t byte_addr) {
 #define TI_RX_BINQ 8   // features searched at once per lane (independent load chains;
                        // 16 measured slower on C3 and C4)
 #endif
-template <typename XT, bool ZB>
-__device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
-                                              int R, int tid) {
+__device__ __forceinline__ uint32_t kpow5(int h) {
+  uint32_t p = 1u;
+  for (int i = 0; i < h; ++i) p *= 5u;
+  return p;
+}
+
+template <typename XT, bool ZB, bool KARY = false>
+__device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, const KArgs& a, int64_t row0,
+                                                   int R, int tid) {
   constexpr int Q = TI_RX_BINQ;
   const XT* tbl = static_cast<const XT*>(a.bin_tbl);
   const int F = a.n_features;
@@ -1362,12 +1369,40 @@ __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a
       tq[q] = (uint32_t)f * tsz;
       k[q] = 1u;
     }
-    for (int s = 0; s < L; ++s) {
-      XT e[Q];
+    if (KARY) {
+      // 5-ary search tree (float32 view): node j holds 4 sorted keys in 16 B,
+      // its children are 5j+1 .. 5j+5; after H levels j - (5^H - 1)/4 is the
+      // number of keys below x.  H gathers instead of L.
+      typedef float f4_t __attribute__((ext_vector_type(4)));
+      const f4_t* t4 = reinterpret_cast<const f4_t*>(a.bin_tbl);
+      const uint32_t nn = (kpow5(a.bin_kary) - 1u) / 4u;   // nodes per feature
 #pragma unroll
-      for (int q = 0; q < Q; ++q) e[q] = tbl[tq[q] + k[q]];
+      for (int q = 0; q < Q; ++q) {
+        tq[q] = (uint32_t)(f0 + q < F ? f0 + q : F - 1) * nn;
+        k[q] = 0u;
+      }
+      for (int s = 0; s < a.bin_kary; ++s) {
+        f4_t e[Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
+        for (int q = 0; q < Q; ++q) e[q] = t4[tq[q] + k[q]];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const float xv = (float)x[q];
+          const uint32_t c = (e[q].x < xv ? 1u : 0u) + (e[q].y < xv ? 1u : 0u) +
+                             (e[q].z < xv ? 1u : 0u) + (e[q].w < xv ? 1u : 0u);
+          k[q] = 5u * k[q] + 1u + c;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q) k[q] = k[q] - nn + tsz;   // as the Eytzinger end: b = 1 + k - tsz
+    } else {
+      for (int s = 0; s < L; ++s) {
+        XT e[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) e[q] = tbl[tq[q] + k[q]];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
+      }
     }
     uint32_t w[Q / 2];
 #pragma unroll
@@ -1397,6 +1432,17 @@ __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a
   if (has_nan && live) *flag = 1;
   __syncthreads();
   return *flag != 0;
+}
+
+// The float32 view searches the 5-ary tables when the host built them
+// (a.bin_kary > 0), every other view the Eytzinger tables.
+template <typename XT, bool ZB>
+__device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
+                                              int R, int tid) {
+  if constexpr (sizeof(XT) == 4) {
+    if (a.bin_kary > 0) return rx_stage_bins_impl<XT, ZB, true>(flag, a, row0, R, tid);
+  }
+  return rx_stage_bins_impl<XT, ZB, false>(flag, a, row0, R, tid);
 }
 
 // Per step every tree's bin read is issued first, then each tree's decision
