@@ -72,6 +72,9 @@ def parse_args(argv=None):
     p.add_argument("--rows4", type=int, default=10_000_000)
     p.add_argument("--config-steps", type=int, default=2)
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
+    p.add_argument("--x-buffers", type=int, default=3,
+                   help="copies of the batch the timed steps rotate through (3 x 112 MB "
+                        "exceeds the 256 MB Infinity Cache)")
     p.add_argument("--host-rows", type=int, default=8_000_000,
                    help="rows of the host-to-host (PCIe-inclusive) C2 leg (0 = skip)")
     return p.parse_args(argv)
@@ -453,11 +456,18 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
     rows, seed = shard_rows(args.rows, rank, world)
     X_host = np.random.default_rng(seed).standard_normal((rows, N_FEAT), dtype=np.float32)
     X = torch.from_numpy(X_host).to(device)
+    # consecutive steps read different copies of the batch: 3 x 112 MB is more
+    # than the 256 MB Infinity Cache, so a step's X comes from HBM, not from
+    # the previous step's cache lines
+    Xs = [X] + [X.clone() for _ in range(max(0, args.x_buffers - 1))]
     out = torch.empty(rows, dtype=torch.float32, device=device)
     sh = torch.cuda.current_stream().cuda_stream if device != "cpu" else 0
+    it = [0]
 
     def step():
-        dev.predict_device(X.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
+        Xi = Xs[it[0] % len(Xs)]
+        it[0] += 1
+        dev.predict_device(Xi.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
                            out.data_ptr(), rows, slot=0, stream=sh)
 
     for _ in range(args.warmup):
@@ -546,7 +556,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
                                    "500 trees depth 8, 1M-row batch per GPU",
                        "rows_per_gpu": rows, "trees": N_TREES, "depth": DEPTH,
                        "features": N_FEAT, "layout": LAYOUT_NAMES.get(info["layout"]),
-                       "parallelism": f"rows sharded x{world}"},
+                       "parallelism": f"rows sharded x{world}", "x_buffers": len(Xs)},
             "roofline": roofline(kernel_ms, rows, LAYOUT_NAMES.get(info["layout"]),
                                  args.pmc_json),
             "cpu_baseline": cpu,
