@@ -1479,6 +1479,21 @@ __device__ __forceinline__ void rx_leaves(const KArgs& a, ACC (&acc)[KMAX], int 
 
 typedef const __attribute__((address_space(4))) uint32_t rx_cu32;   // scalar-loaded tables
 
+#ifndef TI_RX_ADDR2
+#define TI_RX_ADDR2 1
+#endif
+// The bin address of a record step (layouts 6-9): (x & mask) | lane offset
+// inside a tree, the lane's own column of word 0 at its leaf.  The empty asm keeps the
+// compiler from rewriting the select as and / cndmask / or: v_and_or_b32 and
+// one v_cndmask_b32, 2 VALU instead of 3.
+__device__ __forceinline__ uint32_t rx_bin_addr(uint32_t x, bool in, uint32_t lane_off) {
+  uint32_t t = (x & kRxOffMask) | lane_off;
+#if TI_RX_ADDR2
+  asm("" : "+v"(t));
+#endif
+  return in ? t : lane_off;
+}
+
 // The lockstep descent of a group of ILP trees from each lane's current slot
 // (and the record gathered there) to its leaf.
 template <bool ZERO, bool SLOW, int ILP>
@@ -1497,7 +1512,7 @@ __device__ __forceinline__ void rx_descend(const rx_rsrc_t rsrc, const uint32_t 
     uint32_t b[ILP];
 #pragma unroll
     for (int q = 0; q < ILP; ++q)   // a lane at its leaf reads its own column of word 0
-      b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
+      b[q] = lds_u16(rx_bin_addr(rec[q].x, in[q], lane_off));
     any = false;
 #pragma unroll
     for (int q = 0; q < ILP; ++q) {
@@ -1520,7 +1535,7 @@ __device__ __forceinline__ void rx_descend(const rx_rsrc_t rsrc, const uint32_t 
       in[q] = slot[q] < ni[q];
       any |= in[q];
       // a lane at its leaf reads its own column of word 0 (conflict-free)
-      b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
+      b[q] = lds_u16(rx_bin_addr(rec[q].x, in[q], lane_off));
     }
 #pragma unroll
     for (int q = 0; q < ILP; ++q) {
@@ -1637,7 +1652,7 @@ __device__ __forceinline__ void lx_stage(const KArgs& a, ACC (&acc)[KMAX], int t
       for (int q = 0; q < ILP; ++q) {
         in[q] = at[q] < ni8[q];
         any |= in[q];
-        b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
+        b[q] = lds_u16(rx_bin_addr(rec[q].x, in[q], lane_off));
       }
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
@@ -1902,7 +1917,7 @@ __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t
       for (int q = 0; q < ILP; ++q) {
         in[q] = at[q] < ni8[q];
         any |= in[q];
-        b[q] = lds_u16(in[q] ? (rec[q].x & kRxOffMask) | lane_off : lane_off);
+        b[q] = lds_u16(rx_bin_addr(rec[q].x, in[q], lane_off));
       }
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
