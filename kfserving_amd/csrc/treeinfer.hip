@@ -1852,6 +1852,19 @@ KernelFn select_lexplicit(int xdt, int accum, int K, bool z, int ilp) {
   return ti::kernels_df(7, K, true, z, true, ilp);
 }
 
+// Columns per pass of the record layouts' coalesced binning through the stage
+// area (rx_stage_bins): a multiple of 8 that fits `bytes` for R rows, at most
+// the features rounded up to 8; 0 (per-lane row loads) when fewer than 8 fit
+// or TI_BIN_TILED=0.
+int32_t bin_chunk_for(size_t bytes, int R, int xdt, int F) {
+  static const int tiled = env_int("TI_BIN_TILED", 1);
+  if (!tiled) return 0;
+  const size_t per_col = static_cast<size_t>(R) * (xdt == TI_F64 ? 8 : 4);
+  size_t c = (bytes / per_col) & ~size_t(7);
+  c = std::min(c, static_cast<size_t>((F + 7) & ~7));
+  return c >= 8 ? static_cast<int32_t>(c) : 0;
+}
+
 KernelFn select_texplicit(int xdt, int accum, int K, bool z, int ilp) {
   if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(9, K, true, z, true, ilp);
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(9, K, true, z, true, ilp);
@@ -2102,6 +2115,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     lds = std::max(static_cast<size_t>(a.stage_off) + static_cast<size_t>(f->lx_stage_cap), kLxMinLds);
     if (lds > kLdsPerCu || static_cast<int64_t>(kLxPf) * 16 * R < f->lx_stage_cap)
       return fail(TI_ERR_UNSUPPORTED, "staged record layout exceeds LDS");
+    a.bin_chunk = bin_chunk_for(static_cast<size_t>(f->lx_stage_cap), R, xdt, f->F);
     KernelFn fn = select_lexplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
@@ -2130,6 +2144,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     lds = std::max(static_cast<size_t>(a.stage_off) + static_cast<size_t>(f->lx_stage_cap), kLxMinLds);
     if (lds > kLdsPerCu || static_cast<int64_t>(kLxPf) * 16 * R < f->lx_stage_cap)
       return fail(TI_ERR_UNSUPPORTED, "heap-top staged layout exceeds LDS");
+    a.bin_chunk = bin_chunk_for(static_cast<size_t>(f->lx_stage_cap), R, xdt, f->F);
     KernelFn fn = select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
@@ -2160,6 +2175,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     lds = static_cast<size_t>(a.stage_off) + static_cast<size_t>(f->hx_stage) * a.tree_stride;
     if (lds > kLdsPerCu || static_cast<int64_t>(kHxPf) * 16 * R < f->hx_stage * a.tree_stride)
       return fail(TI_ERR_UNSUPPORTED, "heap-top layout exceeds LDS");
+    a.bin_chunk = bin_chunk_for(static_cast<size_t>(f->hx_stage) * a.tree_stride, R, xdt, f->F);
     KernelFn fn = select_hexplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->hx_ilp);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;

@@ -1344,88 +1344,137 @@ __device__ __forceinline__ uint32_t kpow5(int h) {
   return p;
 }
 
-template <typename XT, bool ZB, bool KARY = false>
-__device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, const KArgs& a, int64_t row0,
-                                                   int R, int tid) {
-  constexpr int Q = TI_RX_BINQ;
-  const XT* tbl = static_cast<const XT*>(a.bin_tbl);
+// Search Q consecutive features [f0, f0 + Q) of the lane's row (values x,
+// NaN past the last feature) and store their packed u16 bins in the image
+// (f0 even).  With ZB (zero-missing forests) b2 = 2 b + (x == 0), NaN 0xFFFE.
+template <typename XT, bool ZB, bool KARY, int Q>
+__device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], int f0, int R, int tid,
+                                             bool& has_nan) {
   const int F = a.n_features;
-  const int FC = F < a.n_cols ? F : a.n_cols;
-  const int L = a.bin_L;
-  const uint32_t tsz = 1u << L;
-  const int64_t row = row0 + tid;
-  const bool live = row < a.n_rows;
-  const XT* xr = static_cast<const XT*>(a.X) + (live ? row : a.n_rows - 1) * a.row_stride;
-  bool has_nan = false;
-  if (tid == 0) *flag = 0;
-  for (int f0 = 0; f0 < F; f0 += Q) {
-    XT x[Q];
-    uint32_t tq[Q];   // the feature's table (element offset: 32 bits, not a pointer)
-    uint32_t k[Q];
+  const uint32_t tsz = 1u << a.bin_L;
+  uint32_t tq[Q], k[Q];
+  if (KARY) {
+    // 5-ary search tree (float32 view): node j holds 4 sorted keys in 16 B,
+    // its children are 5j+1 .. 5j+5; after H levels j - (5^H - 1)/4 is the
+    // number of keys below x.  H gathers instead of L.
+    typedef float f4_t __attribute__((ext_vector_type(4)));
+    const f4_t* t4 = reinterpret_cast<const f4_t*>(a.bin_tbl);
+    const uint32_t nn = (kpow5(a.bin_kary) - 1u) / 4u;   // nodes per feature
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const int f = f0 + q < F ? f0 + q : F - 1;
-      x[q] = f0 + q < FC ? zero_map(xr[f], a.lgb_zero_map) : nan_value<XT>();
-      tq[q] = (uint32_t)f * tsz;
-      k[q] = 1u;
+      tq[q] = (uint32_t)(f0 + q < F ? f0 + q : F - 1) * nn;
+      k[q] = 0u;
     }
-    if (KARY) {
-      // 5-ary search tree (float32 view): node j holds 4 sorted keys in 16 B,
-      // its children are 5j+1 .. 5j+5; after H levels j - (5^H - 1)/4 is the
-      // number of keys below x.  H gathers instead of L.
-      typedef float f4_t __attribute__((ext_vector_type(4)));
-      const f4_t* t4 = reinterpret_cast<const f4_t*>(a.bin_tbl);
-      const uint32_t nn = (kpow5(a.bin_kary) - 1u) / 4u;   // nodes per feature
+    for (int s = 0; s < a.bin_kary; ++s) {
+      f4_t e[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) e[q] = t4[tq[q] + k[q]];
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        tq[q] = (uint32_t)(f0 + q < F ? f0 + q : F - 1) * nn;
-        k[q] = 0u;
-      }
-      for (int s = 0; s < a.bin_kary; ++s) {
-        f4_t e[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) e[q] = t4[tq[q] + k[q]];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          const float xv = (float)x[q];
-          const uint32_t c = (e[q].x < xv ? 1u : 0u) + (e[q].y < xv ? 1u : 0u) +
-                             (e[q].z < xv ? 1u : 0u) + (e[q].w < xv ? 1u : 0u);
-          k[q] = 5u * k[q] + 1u + c;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < Q; ++q) k[q] = k[q] - nn + tsz;   // as the Eytzinger end: b = 1 + k - tsz
-    } else {
-      for (int s = 0; s < L; ++s) {
-        XT e[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) e[q] = tbl[tq[q] + k[q]];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
+        const float xv = (float)x[q];
+        const uint32_t c = (e[q].x < xv ? 1u : 0u) + (e[q].y < xv ? 1u : 0u) +
+                           (e[q].z < xv ? 1u : 0u) + (e[q].w < xv ? 1u : 0u);
+        k[q] = 5u * k[q] + 1u + c;
       }
     }
-    uint32_t w[Q / 2];
 #pragma unroll
-    for (int j = 0; j < Q / 2; ++j) w[j] = 0u;
+    for (int q = 0; q < Q; ++q) k[q] = k[q] - nn + tsz;   // as the Eytzinger end: b = 1 + k - tsz
+  } else {
+    const XT* tbl = static_cast<const XT*>(a.bin_tbl);
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const bool nan = x[q] != x[q];
-      const bool zero = ZB && x[q] == XT(0);
-      has_nan |= (nan || zero) && (f0 + q < F);   // the tile needs the slow step
-      uint32_t b = 1u + k[q] - tsz;
-      if (ZB) b = nan ? 0xFFFEu : 2u * b + (zero ? 1u : 0u);
-      else b = nan ? 0xFFFFu : b;
-      w[q / 2] |= b << ((q % 2) * 16);
+      tq[q] = (uint32_t)(f0 + q < F ? f0 + q : F - 1) * tsz;   // element offset, not a pointer
+      k[q] = 1u;
     }
+    for (int s = 0; s < a.bin_L; ++s) {
+      XT e[Q];
 #pragma unroll
-    for (int j = 0; j < Q / 2; ++j) {
-      const int word = f0 / 2 + j;
-      if (word < a.bin_words) {
-        __attribute__((address_space(3))) uint32_t* dst =
-            reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-                static_cast<uintptr_t>((uint32_t)(word * R + tid) * 4u));
-        *dst = w[j];
+      for (int q = 0; q < Q; ++q) e[q] = tbl[tq[q] + k[q]];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
+    }
+  }
+  uint32_t w[Q / 2];
+#pragma unroll
+  for (int j = 0; j < Q / 2; ++j) w[j] = 0u;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const bool nan = x[q] != x[q];
+    const bool zero = ZB && x[q] == XT(0);
+    has_nan |= (nan || zero) && (f0 + q < F);   // the tile needs the slow step
+    uint32_t b = 1u + k[q] - tsz;
+    if (ZB) b = nan ? 0xFFFEu : 2u * b + (zero ? 1u : 0u);
+    else b = nan ? 0xFFFFu : b;
+    w[q / 2] |= b << ((q % 2) * 16);
+  }
+#pragma unroll
+  for (int j = 0; j < Q / 2; ++j) {
+    const int word = f0 / 2 + j;
+    if (word < a.bin_words) {
+      __attribute__((address_space(3))) uint32_t* dst =
+          reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+              static_cast<uintptr_t>((uint32_t)(word * R + tid) * 4u));
+      *dst = w[j];
+    }
+  }
+}
+
+// Bin the tile's rows into the u16 image of layouts 6 to 9.  With a temp area
+// (temp != nullptr: the stage area of layouts 7-9, free until the first stage
+// is committed; a.bin_chunk columns of R rows) and 16-byte-aligned rows, the
+// tile's X goes through it a chunk of columns at a time in coalesced 16-byte
+// loads (a 64-lane load touches 8 lines), and each lane then reads its row's
+// values from LDS; otherwise every lane loads its own row (a load touches 64
+// lines: C3's 400-byte rows made that 0.57 ms of a 5.5 ms kernel).  Returns
+// (uniformly) whether the tile needs the slow step: a NaN, or with ZB an
+// exact 0.
+template <typename XT, bool ZB, bool KARY = false>
+__device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp, const KArgs& a,
+                                                   int64_t row0, int R, int tid) {
+  constexpr int Q = TI_RX_BINQ;
+  const int F = a.n_features;
+  const int FC = F < a.n_cols ? F : a.n_cols;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  const XT* X = static_cast<const XT*>(a.X);
+  bool has_nan = false;
+  if (tid == 0) *flag = 0;
+  constexpr int V = 16 / sizeof(XT);   // elements per 16-byte load
+  const bool tiled = temp != nullptr && a.bin_chunk >= Q && FC == F && (F % V) == 0 &&
+                     ((reinterpret_cast<uintptr_t>(X) | (uintptr_t)(a.row_stride * sizeof(XT))) & 15) == 0;
+  if (tiled) {
+    typedef XT xv_t __attribute__((ext_vector_type(V)));
+    const int64_t left = a.n_rows - row0;
+    const uint32_t rows_here = left < R ? (uint32_t)left : (uint32_t)R;
+    for (int f0 = 0; f0 < F; f0 += a.bin_chunk) {
+      const int kc = (F - f0) < a.bin_chunk ? (F - f0) : a.bin_chunk;
+      const uint32_t kv = (uint32_t)kc / V;
+      __syncthreads();   // temp is free: the previous chunk is searched
+      for (uint32_t e = tid; e < rows_here * kv; e += R) {
+        const uint32_t r = e / kv;
+        const uint32_t cv = e - r * kv;
+        const xv_t v = *reinterpret_cast<const xv_t*>(X + (row0 + r) * a.row_stride + f0 + cv * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) temp[(cv * V + j) * R + r] = zero_map(v[j], a.lgb_zero_map);
       }
+      __syncthreads();
+      for (int c = 0; c < kc; c += Q) {
+        XT x[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) x[q] = c + q < kc ? temp[(c + q) * R + tid] : nan_value<XT>();
+        rx_bin_group<XT, ZB, KARY, Q>(a, x, f0 + c, R, tid, has_nan);
+      }
+    }
+  } else {
+    const XT* xr = X + (live ? row : a.n_rows - 1) * a.row_stride;
+    for (int f0 = 0; f0 < F; f0 += Q) {
+      XT x[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int f = f0 + q < F ? f0 + q : F - 1;
+        x[q] = f0 + q < FC ? zero_map(xr[f], a.lgb_zero_map) : nan_value<XT>();
+      }
+      rx_bin_group<XT, ZB, KARY, Q>(a, x, f0, R, tid, has_nan);
     }
   }
   __syncthreads();   // flag = 0 is visible before any lane sets it
@@ -1438,11 +1487,12 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, const KAr
 // (a.bin_kary > 0), every other view the Eytzinger tables.
 template <typename XT, bool ZB>
 __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
-                                              int R, int tid) {
+                                              int R, int tid, void* temp = nullptr) {
   if constexpr (sizeof(XT) == 4) {
-    if (a.bin_kary > 0) return rx_stage_bins_impl<XT, ZB, true>(flag, a, row0, R, tid);
+    if (a.bin_kary > 0)
+      return rx_stage_bins_impl<XT, ZB, true>(flag, static_cast<XT*>(temp), a, row0, R, tid);
   }
-  return rx_stage_bins_impl<XT, ZB, false>(flag, a, row0, R, tid);
+  return rx_stage_bins_impl<XT, ZB, false>(flag, static_cast<XT*>(temp), a, row0, R, tid);
 }
 
 // Per step every tree's bin read is issued first, then each tree's decision
@@ -1692,7 +1742,7 @@ __global__ void __launch_bounds__(512) lexplicit_predict_kernel(const KArgs a) {
   auto n16_of = [&](int s) { return (int)((((rx_base[sst[s + 1]] << 3) + 15u) & ~15u) - lo_of(s)) >> 4; };
   u32x4 pf[PF];
   prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(recs + lo_of(0)), n16_of(0), tid, R);
-  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid);
+  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid, stage);
   const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
   ACC acc[KMAX];
   init_acc(acc, a);
@@ -1820,7 +1870,7 @@ __global__ void __launch_bounds__(512) hexplicit_predict_kernel(const KArgs a) {
   u32x4 pf[PF];
   prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees),
                  (int)(((int64_t)(T < S ? T : S) * stride) >> 4), tid, R);
-  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid);
+  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid, stage);
   const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
   ACC acc[KMAX];
   init_acc(acc, a);
@@ -1955,7 +2005,7 @@ __global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
   auto n16_of = [&](int s) { return (int)((tx_off[sst[s + 1]] - tx_off[sst[s]]) >> 4); };
   u32x4 pf[PF];
   prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(0)), n16_of(0), tid, R);
-  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid);
+  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid, stage);
   const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
   ACC acc[KMAX];
   init_acc(acc, a);
