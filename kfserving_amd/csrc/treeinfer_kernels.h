@@ -1347,7 +1347,7 @@ __device__ __forceinline__ uint32_t kpow5(int h) {
 // Search Q consecutive features [f0, f0 + Q) of the lane's row (values x,
 // NaN past the last feature) and store their packed u16 bins in the image
 // (f0 even).  With ZB (zero-missing forests) b2 = 2 b + (x == 0), NaN 0xFFFE.
-template <typename XT, bool ZB, bool KARY, int Q>
+template <typename XT, bool ZB, bool KARY, int Q, bool SROOT = false>
 __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], int f0, int R, int tid,
                                              bool& has_nan) {
   const int F = a.n_features;
@@ -1365,7 +1365,20 @@ __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], i
       tq[q] = (uint32_t)(f0 + q < F ? f0 + q : F - 1) * nn;
       k[q] = 0u;
     }
-    for (int s = 0; s < a.bin_kary; ++s) {
+    int s0 = 0;
+    if (SROOT) {   // the root, the same node for every lane, as a scalar load
+      typedef const __attribute__((address_space(4))) f4_t cf4_t;
+      cf4_t* s4 = reinterpret_cast<cf4_t*>(reinterpret_cast<uintptr_t>(a.bin_tbl));
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const f4_t e = s4[tq[q]];
+        const float xv = (float)x[q];
+        k[q] = 1u + (e.x < xv ? 1u : 0u) + (e.y < xv ? 1u : 0u) + (e.z < xv ? 1u : 0u) +
+               (e.w < xv ? 1u : 0u);
+      }
+      s0 = 1;
+    }
+    for (int s = s0; s < a.bin_kary; ++s) {
       f4_t e[Q];
 #pragma unroll
       for (int q = 0; q < Q; ++q) e[q] = t4[tq[q] + k[q]];
@@ -1428,7 +1441,7 @@ __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], i
 // lines: C3's 400-byte rows made that 0.57 ms of a 5.5 ms kernel).  Returns
 // (uniformly) whether the tile needs the slow step: a NaN, or with ZB an
 // exact 0.
-template <typename XT, bool ZB, bool KARY = false>
+template <typename XT, bool ZB, bool KARY = false, bool SROOT = false>
 __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp, const KArgs& a,
                                                    int64_t row0, int R, int tid) {
   constexpr int Q = TI_RX_BINQ;
@@ -1462,7 +1475,7 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
         XT x[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) x[q] = c + q < kc ? temp[(c + q) * R + tid] : nan_value<XT>();
-        rx_bin_group<XT, ZB, KARY, Q>(a, x, f0 + c, R, tid, has_nan);
+        rx_bin_group<XT, ZB, KARY, Q, SROOT>(a, x, f0 + c, R, tid, has_nan);
       }
     }
   } else {
@@ -1474,7 +1487,7 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
         const int f = f0 + q < F ? f0 + q : F - 1;
         x[q] = f0 + q < FC ? zero_map(xr[f], a.lgb_zero_map) : nan_value<XT>();
       }
-      rx_bin_group<XT, ZB, KARY, Q>(a, x, f0, R, tid, has_nan);
+      rx_bin_group<XT, ZB, KARY, Q, SROOT>(a, x, f0, R, tid, has_nan);
     }
   }
   __syncthreads();   // flag = 0 is visible before any lane sets it
@@ -1485,12 +1498,14 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
 
 // The float32 view searches the 5-ary tables when the host built them
 // (a.bin_kary > 0), every other view the Eytzinger tables.
-template <typename XT, bool ZB>
+// SROOT: the 5-ary root as a scalar load (layout 8: C4 2.17 -> 2.13 ms; on
+// layout 9 it cost C3 0.7 %, profiles/r2_kary_root_sweep.jsonl)
+template <typename XT, bool ZB, bool SROOT = false>
 __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
                                               int R, int tid, void* temp = nullptr) {
   if constexpr (sizeof(XT) == 4) {
     if (a.bin_kary > 0)
-      return rx_stage_bins_impl<XT, ZB, true>(flag, static_cast<XT*>(temp), a, row0, R, tid);
+      return rx_stage_bins_impl<XT, ZB, true, SROOT>(flag, static_cast<XT*>(temp), a, row0, R, tid);
   }
   return rx_stage_bins_impl<XT, ZB, false>(flag, static_cast<XT*>(temp), a, row0, R, tid);
 }
@@ -1870,7 +1885,7 @@ __global__ void __launch_bounds__(512) hexplicit_predict_kernel(const KArgs a) {
   u32x4 pf[PF];
   prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees),
                  (int)(((int64_t)(T < S ? T : S) * stride) >> 4), tid, R);
-  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid, stage);
+  const bool slow = rx_stage_bins<XT, ZERO, true>(flag, a, row0, R, tid, stage);
   const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
   ACC acc[KMAX];
   init_acc(acc, a);
