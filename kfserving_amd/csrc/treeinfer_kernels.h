@@ -794,6 +794,35 @@ __device__ __forceinline__ void commit_n(const u32x4 (&pf)[PF], u32x4* __restric
   }
 }
 
+// Layout 9's stage copies: as prefetch_n / commit_n, but the loads address
+// the uniform base with a 32-bit byte offset (the scalar-base form of
+// global_load: an index clamp and a shift each) and the commit writes every
+// word unconditionally (a clamped lane stores the last word's own value
+// again: no compare and branch per store).  C3 5.41 -> 5.34 ms; the same
+// copies measured about 1 % slower on C2 and C4, which keep the others
+// (profiles/r2_copy_sweep.jsonl).
+template <int PF>
+__device__ __forceinline__ void prefetch_u(u32x4 (&pf)[PF], const u32x4* __restrict__ src,
+                                           int n16, int tid, int R) {
+  const unsigned char* base = reinterpret_cast<const unsigned char*>(src);
+  const uint32_t last = (uint32_t)n16 - 1u;
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)(u * R);
+    pf[u] = *reinterpret_cast<const u32x4*>(base + (i < last ? i : last) * 16u);
+  }
+}
+template <int PF>
+__device__ __forceinline__ void commit_u(const u32x4 (&pf)[PF], u32x4* __restrict__ dst, int n16,
+                                         int tid, int R) {
+  const uint32_t last = (uint32_t)n16 - 1u;
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)(u * R);
+    dst[i < last ? i : last] = pf[u];
+  }
+}
+
 // LDS: [bin image (bin_words * R u32)] [flag word] ... [stage area at
 // stage_off: S tree records, also the binning temp].
 template <typename XT, typename ACC, int KMAX, bool B16, int PF>
@@ -2019,7 +2048,7 @@ __global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
   auto lo_of = [&](int s) { return tx_off[sst[s]]; };   // trees start 16-byte aligned
   auto n16_of = [&](int s) { return (int)((tx_off[sst[s + 1]] - tx_off[sst[s]]) >> 4); };
   u32x4 pf[PF];
-  prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(0)), n16_of(0), tid, R);
+  prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(0)), n16_of(0), tid, R);
   const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid, stage);
   const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
   ACC acc[KMAX];
@@ -2028,10 +2057,10 @@ __global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
     const int t0 = (int)sst[s], t1 = (int)sst[s + 1];
     const uint32_t lo = lo_of(s);
     __syncthreads();   // the previous stage's walk is over
-    commit_n<PF>(pf, stage, n16_of(s), tid, R);
+    commit_u<PF>(pf, stage, n16_of(s), tid, R);
     __syncthreads();
     const int sn = s + 1 < NS ? s + 1 : s;
-    prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(sn)), n16_of(sn), tid, R);
+    prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(sn)), n16_of(sn), tid, R);
     const uint32_t sbase = (uint32_t)a.stage_off - lo;   // LDS address = sbase + image byte
     if (slow) {
       if (vis) tx_stage<ACC, KMAX, ZERO, true, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
