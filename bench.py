@@ -13,20 +13,31 @@ Also reported (rank 0):
                   4).  achieved = VALU wave-instructions per launch (committed
                   rocprofv3 PMC pass of the same kernel, profiles/pmc_c2.json)
                   / the kernel's average duration from HIP events on the launch
-                  stream; peak = 1,024 SIMDs x 2.4 GHz / 4 cycles per wave64
-                  VALU instruction.  The HBM view is kept beside it:
-                  compulsory bytes (X + out) and counter bytes (FETCH_SIZE +
-                  WRITE_SIZE) per launch as fractions of 8 TB/s.
+                  stream; peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64
+                  VALU instruction (MI355X_MICROARCH.md: a wave64 VALU
+                  instruction issues over 2 cycles on a SIMD-32).  Beside it:
+                  `peak_mix`, the ceiling of the walk's own instruction mix
+                  measured by scripts/micro/valu_rate.hip at the chip's
+                  effective clock (profiles/r3_valu_rate.jsonl), and
+                  `profiled`, the same count priced on the PMC run's own
+                  cycles (GRBM_GUI_ACTIVE per XCD; its clock = those cycles /
+                  its kernel duration).  The HBM view is kept beside it:
+                  compulsory bytes (X + out) and counter bytes (FETCH_SIZE x 2
+                  + WRITE_SIZE) per launch as fractions of 8 TB/s.
   cpu_baseline -- the C/OpenMP restatement of xgboost 0.82's predict loop
                   (oracle/c/tree_port.c, kind "port": xgboost is not installed)
                   timed on this host on a bounded sample of the same rows.
-  c3, c4       -- the other named GPU configs at their BASELINE sizes, row-
+  c3, c3_f64, c4 -- the other named GPU configs at their BASELINE sizes, row-
                   sharded over the ranks (strong scaling, max-over-ranks wall):
-                  C3 LightGBM leaf-wise 1000 x 255 leaves, F = 100, 100M rows;
-                  C4 sklearn RandomForestRegressor 200 x depth 16, F = 64, 10M
-                  rows (the cached fit of scripts/make_c4_model.py).  Each
-                  carries a `roofline` (config_roofline): the busiest of VALU
-                  issue, LDS array and TD cycles, from a committed PMC pass.
+                  C3 LightGBM leaf-wise 1000 x 255 leaves, F = 100, 100M rows,
+                  float32 X (c3) and float64 X (c3_f64: what lgbserver's
+                  DataFrame path feeds, lgbserver/model.py:46-51); C4 sklearn
+                  RandomForestRegressor 200 x depth 16, F = 64, 10M rows (the
+                  cached fit of scripts/make_c4_model.py).  Each carries a
+                  `roofline` (config_roofline): the busiest of VALU issue, LDS
+                  array and TD cycles of a committed PMC pass, priced on that
+                  pass's own cycles.  C4's cpu_baseline is sklearn's own
+                  RandomForestRegressor.predict (kind "library").
   batched_latency, nan_variant -- see the functions below.
 """
 from __future__ import annotations
@@ -44,10 +55,12 @@ sys.path.insert(0, ROOT)
 
 N_TREES, DEPTH, N_FEAT, ROWS = 500, 8, 28, 1_000_000
 HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md)
-SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 4.0
-VALU_PEAK = SIMDS * CLOCK_HZ / VALU_CYCLES     # wave64 VALU instructions / s
-LAYOUT_NAMES = {0: "heap", 1: "explicit", 2: "compact", 3: "bheap", 4: "bexplicit",
-                5: "sexplicit", 6: "rexplicit", 7: "lexplicit",
+SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 2.0   # MI355X_MICROARCH.md: wave64 over 2 cycles
+VALU_PEAK = SIMDS * CLOCK_HZ / VALU_CYCLES     # wave64 VALU instructions / s (1,228.8 G)
+VALU_RATE_JSONL = os.path.join(ROOT, "profiles", "r3_valu_rate.jsonl")
+# the binned-heap walk's step (ti_forest_info.walk) -> its row in VALU_RATE_JSONL
+WALK_STEPS = {0: "step r2", 1: "step fixed (and_or, and, cmp_sdwa, cndmask)"}
+LAYOUT_NAMES = {0: "heap", 1: "explicit", 3: "bheap", 6: "rexplicit", 7: "lexplicit",
                 8: "hexplicit", 9: "texplicit"}
 
 
@@ -66,7 +79,7 @@ def parse_args(argv=None):
     p.add_argument("--latency-qps", type=float, default=10000.0,
                    help="offered requests/s for the batched-latency leg (0 = skip)")
     p.add_argument("--latency-seconds", type=float, default=3.0)
-    p.add_argument("--configs", default="c3,c4",
+    p.add_argument("--configs", default="c3,c3_f64,c4",
                    help="other named configs to time after the headline ('' = none)")
     p.add_argument("--rows3", type=int, default=100_000_000)
     p.add_argument("--rows4", type=int, default=10_000_000)
@@ -156,24 +169,41 @@ def cpu_baseline(trees, ti, X_host, target_s):
                       f"{dt:.1f} s"}
 
 
-def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str):
+def valu_step_rate(op_prefix: str, waves_per_simd: int = 8, path: str = VALU_RATE_JSONL):
+    """The measured issue cost of one walk step (scripts/micro/valu_rate.hip
+    rows "step ..."): (VALU per step, cycles per step per SIMD, clock GHz)."""
+    try:
+        with open(path) as fh:
+            rows = [json.loads(l) for l in fh if l.strip().startswith("{")]
+    except (OSError, ValueError):
+        return None
+    for r in rows:
+        if r["op"].startswith(op_prefix) and r["waves_per_simd"] == waves_per_simd:
+            return r
+    return None
+
+
+def load_pmc(path: str):
+    try:
+        with open(path) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return None
+
+
+def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str, step_op: str = None):
     """Binding-resource roofline of the C2 kernel (see the module docstring)."""
-    pmc = None
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as fh:
-                pmc = json.load(fh)
-        except (OSError, ValueError):
-            pmc = None
+    pmc = load_pmc(pmc_path)
     if pmc and not (pmc.get("rows") == rows and pmc.get("workload") == "c2"
-                    and pmc.get("layout") == layout and "valu_insts_per_launch" in pmc):
+                    and pmc.get("layout") == layout and "valu_insts_per_launch" in pmc
+                    and (step_op is None or pmc.get("walk_step") == step_op)):
         pmc = None       # a pass of another kernel / size does not describe this one
     t = kernel_ms * 1e-3
     compulsory = (4 * N_FEAT + 4) * rows
     out = {"bound": "valu_issue", "unit": "Ginst/s", "peak": VALU_PEAK / 1e9,
            "achieved": None, "frac": None, "traffic": None, "kernel_ms": kernel_ms,
            "peak_basis": f"{SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz / {VALU_CYCLES:g} cycles per "
-                         "wave64 VALU instruction",
+                         "wave64 VALU instruction (MI355X_MICROARCH.md)",
            "hbm_compulsory_bytes": compulsory,
            "hbm_compulsory_frac": compulsory / t / HBM_PEAK}
     if pmc:
@@ -186,7 +216,25 @@ def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str):
             out["hbm_counter_frac"] = out["traffic"] / t / HBM_PEAK
             out["traffic_over_compulsory"] = out["traffic"] / (compulsory + pmc.get(
                 "model_bytes", 0))
+        cyc = pmc.get("gui_active_cycles_per_xcd")
+        if cyc:
+            out["profiled"] = {
+                "frac": valu * VALU_CYCLES / (SIMDS * cyc),
+                "kernel_ms": (pmc.get("profiled_kernel_ns") or 0) * 1e-6 or None,
+                "clock_GHz": pmc.get("profiled_clock_GHz"),
+                "basis": "VALU x 2 cycles / (1,024 SIMDs x GRBM_GUI_ACTIVE/8 of the PMC pass)"}
         out["pmc_source"] = pmc.get("source")
+    if step_op:
+        st = valu_step_rate(step_op)
+        if st:
+            mix = st["valu_per_step"] / st["cycles_per_step_per_simd"] * SIMDS * CLOCK_HZ
+            out["peak_mix"] = mix / 1e9
+            out["peak_mix_basis"] = (f"walk step '{st['op']}': {st['valu_per_step']} VALU in "
+                                     f"{st['cycles_per_step_per_simd']:.2f} cycles per SIMD at 8 "
+                                     f"waves/SIMD (profiles/r3_valu_rate.jsonl), x {SIMDS} SIMDs "
+                                     f"x {CLOCK_HZ / 1e9} GHz")
+            if out["achieved"]:
+                out["frac_mix"] = out["achieved"] * 1e9 / mix
     return out
 
 
@@ -194,31 +242,43 @@ CUS = 256
 
 
 def config_roofline(kernel_ms: float, rows: int, layout: str, workload: str, pmc_path: str):
-    """Binding-resource roofline of a C3 / C4 launch from a committed PMC pass of
-    the same kernel at 1M rows (scripts/r2_cfgprof.sh -> scripts/make_cfg_pmc_json.py),
-    scaled by rows.  Three issue-type resources are priced, each against its
-    own peak: VALU issue (wave64 instructions, 4 cycles each, 1,024 SIMDs),
-    the LDS array (cycles, one array per CU) and the TD (vector-memory data
-    path, busy cycles per CU: what a node gather occupies).  `bound` is the
-    busiest of the three; the HBM compulsory rate is reported beside it."""
-    try:
-        with open(pmc_path) as fh:
-            pmc = json.load(fh)
-    except (OSError, ValueError):
-        return None
-    if pmc.get("workload") != workload or pmc.get("layout") != layout:
+    """Binding-resource roofline of a C3 / C4 launch from a committed PMC pass
+    of the same kernel at 1M rows (scripts/kernel_pmc.sh ->
+    scripts/make_pmc_json.py).  Three issue-type resources are priced, each
+    against its own peak per cycle: VALU issue (wave64 instructions at 2
+    cycles on 1,024 SIMDs), the LDS array (cycles, one array per CU) and the
+    TD (vector-memory data path, busy cycles per CU: what a node gather
+    occupies).  `frac` is priced on the PMC run's own cycles
+    (GRBM_GUI_ACTIVE per XCD: its duration at its clock), never on another
+    run's time; `fracs_bench` re-prices the per-row counts on this run's
+    kernel time at the nominal 2.4 GHz.  `bound` is the busiest resource."""
+    pmc = load_pmc(pmc_path)
+    if not pmc or pmc.get("workload") != workload or pmc.get("layout") != layout:
         return None       # a pass of another kernel does not describe this one
+    cyc = pmc.get("gui_active_cycles_per_xcd")
+    # (count, units, the cycles of the pass that counted it)
+    counts = {"valu_issue": (pmc["valu_insts_per_launch"] * VALU_CYCLES, SIMDS,
+                             pmc.get("valu_pass_cycles_per_xcd") or cyc)}
+    if pmc.get("lds_idx_active_per_launch"):
+        counts["lds_array"] = (pmc["lds_idx_active_per_launch"], CUS,
+                               pmc.get("lds_pass_cycles_per_xcd") or cyc)
+    if pmc.get("td_busy_per_launch"):
+        counts["td_busy"] = (pmc["td_busy_per_launch"], CUS, pmc.get("td_pass_cycles_per_xcd") or cyc)
+    fr = {k: c / (u * cy) for k, (c, u, cy) in counts.items() if cy}
     t = kernel_ms * 1e-3
     scale = rows / pmc["rows"]
-    fr = {"valu_issue": pmc["valu_insts_per_launch"] * scale * VALU_CYCLES / (SIMDS * CLOCK_HZ * t)}
-    if pmc.get("lds_idx_active_per_launch"):
-        fr["lds_array"] = pmc["lds_idx_active_per_launch"] * scale / (CUS * CLOCK_HZ * t)
-    if pmc.get("td_busy_per_launch"):
-        fr["td_busy"] = pmc["td_busy_per_launch"] * scale / (CUS * CLOCK_HZ * t)
-    bound = max(fr, key=fr.get)
-    out = {"bound": bound, "frac": fr[bound], "fracs": fr,
-           "basis": "per-row counts of the PMC pass x rows / (resource peak x kernel time)",
+    fb = {k: c * scale / (u * CLOCK_HZ * t) for k, (c, u, _) in counts.items()}
+    src = fr or fb
+    bound = max(src, key=src.get)
+    out = {"bound": bound, "frac": src[bound], "fracs": src, "fracs_bench": fb,
+           "basis": ("counts of the PMC pass / (units x that pass's GRBM_GUI_ACTIVE per XCD); "
+                     "VALU at 2 cycles per wave64 instruction"),
+           "profiled_kernel_ms": (pmc.get("profiled_kernel_ns") or 0) * 1e-6 or None,
+           "profiled_clock_GHz": pmc.get("profiled_clock_GHz"),
            "pmc_source": pmc.get("source"), "pmc_rows": pmc["rows"]}
+    for k in ("lds_bank_conflict_frac", "wait_frac", "l2_hit_rate", "waves_per_simd"):
+        if pmc.get(k) is not None:
+            out[k] = pmc[k]
     if pmc.get("hbm_bytes_per_launch"):
         out["traffic"] = pmc["hbm_bytes_per_launch"] * scale
     return out
@@ -318,16 +378,18 @@ def host_to_host(dev, X_host, rows, reps=3):
 
 
 # ------------------------------------------------------------ other configs
-def device_normal(rows, cols, seed, device):
-    """X ~ N(0,1) float32 generated on the device in 8M-row chunks (seed, chunk)."""
+def device_normal(rows, cols, seed, device, dtype="float32"):
+    """X ~ N(0,1) generated on the device in 8M-row chunks (seed, chunk), as
+    float32 or float64 (the float64 draws are not the float32 ones widened)."""
     import torch
-    X = torch.empty((rows, cols), dtype=torch.float32, device=device)
+    dt = torch.float64 if dtype == "float64" else torch.float32
+    X = torch.empty((rows, cols), dtype=dt, device=device)
     chunk = 8 << 20
     for i, lo in enumerate(range(0, rows, chunk)):
         g = torch.Generator(device=device)
         g.manual_seed(seed * 1000003 + i)
         hi = min(rows, lo + chunk)
-        X[lo:hi] = torch.randn((hi - lo, cols), generator=g, device=device, dtype=torch.float32)
+        X[lo:hi] = torch.randn((hi - lo, cols), generator=g, device=device, dtype=dt)
     return X
 
 
@@ -361,20 +423,21 @@ def c4_forest():
 
 
 def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_sync,
-               make_engine, cpu_fn=None, pmc_workload=None, pmc_path=None):
+               make_engine, cpu_fn=None, pmc_workload=None, pmc_path=None, dtype="float32"):
     """Strong scaling: this rank's block of the batch, K steps, max-over-ranks wall."""
     import torch
-    from kfserving_amd.forest import OUT_PREDICT, TI_F32
+    from kfserving_amd.forest import OUT_PREDICT, TI_F32, TI_F64
     lo, hi = strong_shard(total_rows, rank, world)
     rows = hi - lo
     eng = make_engine(forest)
-    X = device_normal(rows, n_feat, seed + rank, device)
+    X = device_normal(rows, n_feat, seed + rank, device, dtype)
+    xdt = TI_F64 if dtype == "float64" else TI_F32
     out = torch.empty(rows * forest.output_width(OUT_PREDICT),
                       dtype=torch.float64 if forest.accum_dtype else torch.float32, device=device)
     sh = torch.cuda.current_stream().cuda_stream if device != "cpu" else 0
 
     def step():
-        eng.predict_device(X.data_ptr(), TI_F32, rows, n_feat, n_feat, OUT_PREDICT,
+        eng.predict_device(X.data_ptr(), xdt, rows, n_feat, n_feat, OUT_PREDICT,
                            out.data_ptr(), out.numel(), slot=0, stream=sh)
 
     step()
@@ -384,43 +447,87 @@ def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_
     wall = max_over_ranks(wall, device)
     res = None
     if rank == 0:
-        res = {"rows": total_rows, "rows_per_gpu": rows, "scaling": "strong",
+        res = {"rows": total_rows, "rows_per_gpu": rows, "scaling": "strong", "dtype": dtype,
                "steps": args.config_steps, "rows_per_s": total_rows * args.config_steps / wall,
                "ms_per_step": wall / args.config_steps * 1e3, "kernel_ms_rank0": kms,
                "layout": LAYOUT_NAMES.get(eng.info()["layout"]),
-               "compulsory_GBps": ((4 * n_feat + out.element_size()) * rows / (kms * 1e-3) / 1e9
-                                   if kms else None)}
+               "compulsory_GBps": ((X.element_size() * n_feat + out.element_size()) * rows
+                                   / (kms * 1e-3) / 1e9 if kms else None)}
         if pmc_path and kms:
             res["roofline"] = config_roofline(kms, rows, res["layout"], pmc_workload, pmc_path)
         if cpu_fn is not None and world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_fn(X[:min(rows, 20_000)].cpu().numpy())
+            res["cpu_baseline"] = cpu_fn(lambda n: X[:min(rows, n)].cpu().numpy())
     del X, out
     eng.close()
+    if device != "cpu":
+        torch.cuda.empty_cache()
     return res
 
 
-def c3_cpu(trees):
-    def fn(Xs):
+def _scaled_sample(fn, take, target_s, probe=20_000, cap=4_000_000):
+    """Time fn on a probe, then on a sample sized for about target_s seconds."""
+    Xp = take(probe)
+    t0 = time.perf_counter()
+    fn(Xp)
+    rate = Xp.shape[0] / max(time.perf_counter() - t0, 1e-9)
+    Xs = take(int(min(cap, max(probe, rate * target_s))))
+    t0 = time.perf_counter()
+    fn(Xs)
+    return Xs.shape[0], time.perf_counter() - t0
+
+
+def c3_cpu(trees, target_s, dtype="float32"):
+    def fn(take):
         from oracle import port
-        t0 = time.perf_counter()
-        port.lgb_predict_raw(trees, 1, 100, Xs.astype(np.float64))
-        dt = time.perf_counter() - t0
-        return {"value": Xs.shape[0] / dt, "unit": "rows/s", "cores": port.num_threads(),
-                "kind": "port", "sample": f"{Xs.shape[0]} rows, oracle/c/tree_port.c "
-                                          f"(lightgbm predict loop restated), {dt:.2f} s"}
+        n, dt = _scaled_sample(lambda Xs: port.lgb_predict_raw(trees, 1, 100, Xs.astype(np.float64)),
+                               take, target_s)
+        return {"value": n / dt, "unit": "rows/s", "cores": port.num_threads(),
+                "kind": "port", "sample": f"{n} rows of the same {dtype} batch, "
+                                          "oracle/c/tree_port.c (lightgbm predict loop restated, "
+                                          f"OpenMP), {dt:.1f} s"}
     return fn
 
 
-def c4_cpu(raw_trees):
-    def fn(Xs):
+def host_threads() -> int:
+    """The host threads this process may use: OMP_NUM_THREADS when set (the
+    GPU box sets it to the box's CPU share, 16), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def c4_cpu(raw_trees, target_s):
+    """C4's CPU baseline is the library: sklearn's own RandomForestRegressor
+    .predict (sklearnserver/model.py:46-51) on the fitted forest rebuilt from
+    its cached arrays (scripts/make_c4_model.sklearn_estimator, checked bit for
+    bit against the fitted estimator's answers), n_jobs = the host threads.
+    The C restatement is timed beside it as `cpu_baseline_port`."""
+    def fn(take):
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import make_c4_model as mk
+        res = {}
+        if os.path.exists(mk.MODEL) and os.path.exists(mk.CHECK):
+            est = mk.sklearn_estimator()
+            same = mk.check(est)
+            thr = host_threads()
+            est.set_params(n_jobs=thr)
+            n, dt = _scaled_sample(est.predict, take, target_s, probe=4096)
+            import sklearn
+            res["cpu_baseline"] = {
+                "value": n / dt, "unit": "rows/s", "cores": thr, "kind": "library",
+                "sample": f"{n} rows of the same float32 batch, sklearn {sklearn.__version__} "
+                          f"RandomForestRegressor.predict(n_jobs={thr}) on the cached fit "
+                          f"(rebuilt from its arrays; equal to the fitted estimator on the "
+                          f"check rows: {same}), {dt:.1f} s"}
         from oracle import port
-        n = min(Xs.shape[0], 5000)
-        t0 = time.perf_counter()
-        port.sk_predict(raw_trees, 1, 64, Xs[:n])
-        dt = time.perf_counter() - t0
-        return {"value": n / dt, "unit": "rows/s", "cores": port.num_threads(), "kind": "port",
-                "sample": f"{n} rows, oracle/c/tree_port.c (sklearn forest predict "
-                          f"restated), {dt:.2f} s"}
+        n, dt = _scaled_sample(lambda Xs: port.sk_predict(raw_trees, 1, 64, Xs), take,
+                               min(target_s, 5.0), probe=4096)
+        res["cpu_baseline_port"] = {
+            "value": n / dt, "unit": "rows/s", "cores": port.num_threads(), "kind": "port",
+            "sample": f"{n} rows, oracle/c/tree_port.c (sklearn forest predict restated), "
+                      f"{dt:.1f} s"}
+        return res
     return fn
 
 
@@ -510,20 +617,24 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
 
     configs = {}
     for name in [c.strip() for c in args.configs.split(",") if c.strip()]:
-        if name == "c3":
+        if name in ("c3", "c3_f64"):
             f3, t3, src = c3_forest()
+            dt = "float64" if name == "c3_f64" else "float32"
             r = run_config(f3, 100, args.rows3, 3, args, world, rank, device, dev_sync,
-                           make_engine, c3_cpu(t3), "c3",
-                           os.path.join(ROOT, "profiles", "r2_c3_pmc.json"))
+                           make_engine, c3_cpu(t3, args.cpu_seconds / 2, dt), name,
+                           os.path.join(ROOT, "profiles", f"r3_{name}_pmc.json"), dt)
             if r is not None:
-                r.update(config="C3 LightGBM leaf-wise 1000 trees x 255 leaves, 100 features, "
-                                "float32 input, float64 sigmoid of the raw score", model=src)
+                r.update(config=f"C3 LightGBM leaf-wise 1000 trees x 255 leaves, 100 features, "
+                                f"{dt} input, float64 sigmoid of the raw score", model=src)
         elif name == "c4":
             f4, raw4, src = c4_forest()
             r = run_config(f4, 64, args.rows4, 2, args, world, rank, device, dev_sync,
-                           make_engine, c4_cpu(raw4), "c4",
-                           os.path.join(ROOT, "profiles", "r2_c4_pmc.json"))
+                           make_engine, c4_cpu(raw4, args.cpu_seconds / 2), "c4",
+                           os.path.join(ROOT, "profiles", "r3_c4_pmc.json"))
             if r is not None:
+                cb = r.pop("cpu_baseline", None)
+                if cb:
+                    r.update(cb)
                 r.update(config="C4 sklearn RandomForestRegressor 200 trees max_depth 16, "
                                 "64 features, float32 input, float64 mean", model=src)
         else:
@@ -558,7 +669,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
                        "features": N_FEAT, "layout": LAYOUT_NAMES.get(info["layout"]),
                        "parallelism": f"rows sharded x{world}", "x_buffers": len(Xs)},
             "roofline": roofline(kernel_ms, rows, LAYOUT_NAMES.get(info["layout"]),
-                                 args.pmc_json),
+                                 args.pmc_json, WALK_STEPS.get(info.get("walk"))),
             "cpu_baseline": cpu,
             "batched_latency": latency,
             "nan_variant": nan_variant,

@@ -152,10 +152,10 @@ typedef struct ti_forest ti_forest;   /* opaque, owns device memory */
 /* Layout the engine chose for a forest (diagnostics, bench byte models). */
 typedef struct ti_forest_info {
   int32_t layout;             /* 0 heap (complete, LDS-staged), 1 explicit nodes,
-                                 2 compact, 3 binned heap, 4 binned explicit, 5 staged
-                                 binned explicit, 6 record explicit (gathered), 7 staged
+                                 3 binned heap, 6 record explicit (gathered), 7 staged
                                  records, 8 heap tops + gathered records, 9 heap tops +
-                                 staged records               */
+                                 staged records (2, 4 and 5 were
+                                 retired in round 3)                                 */
   int32_t depth;              /* heap depth D, or max depth for explicit             */
   int32_t n_trees;
   int32_t n_groups;
@@ -163,6 +163,9 @@ typedef struct ti_forest_info {
   int32_t n_devices;
   int64_t device_bytes;       /* forest bytes resident per device                   */
   int64_t tree_stride_bytes;  /* heap layout: bytes per staged tree                 */
+  int32_t walk;               /* binned heap walk of float32 input: 0 indexed step
+                                 (5 VALU), 1 fixed-layout step (4 VALU)  */
+  int32_t bin_bits;           /* 8 or 16: bin width of the float32 image (0: none)   */
 } ti_forest_info;
 
 /* Upload the forest to each listed device (HIP device ordinals).  HIP is

@@ -431,8 +431,8 @@ extern "C" int kf_parse_instances_mt(const char* body, int64_t len, double* out,
           }
           if (!s.eat(',')) return;
           s.ws();
-          if (s.p == limit) {   // the next slice's first row
-            ok[i] = r == r0[i + 1];
+          if (s.p == limit) {   // the next slice's first row; a comma must be followed by a row,
+            ok[i] = limit != e && r == r0[i + 1];   // so at the body's end it is a trailing comma
             return;
           }
           if (s.p > limit) return;

@@ -406,18 +406,10 @@ struct DeviceForest {
   int32_t* exp_leaf_ids = nullptr;
   uint32_t* cat_words = nullptr;
   int32_t* tree_group = nullptr;
-  // compact layout
-  unsigned char* cpt_img[2] = {nullptr, nullptr};
-  int64_t* cpt_off[2] = {nullptr, nullptr};
-  int32_t* cpt_stage[2] = {nullptr, nullptr};
-  int32_t* cpt_nint = nullptr;
-  int32_t* cpt_depth = nullptr;
-  int32_t* cpt_root = nullptr;
   // binned heap layout: one image + threshold tables per input dtype
   unsigned char* bh_img[2] = {nullptr, nullptr};
   unsigned char* bh_tbl[2] = {nullptr, nullptr};
-  // binned explicit layout: rank-coded nodes + tables per input dtype
-  ExpNode* bx_nodes[2] = {nullptr, nullptr};
+  // record layouts (6-9): rank tables per input dtype
   unsigned char* bx_tbl[2] = {nullptr, nullptr};
   // record explicit layout
   uint2* rx_recs[2] = {nullptr, nullptr};
@@ -467,45 +459,19 @@ struct ti_forest {
   int32_t depth = 0;
   int64_t stride32 = 0, stride64 = 0;
   int32_t rows32 = 256, rows64 = 256;   // heap: rows per tile of each image (0 = HBM features)
-  // compact layout (2): one image per input dtype
-  struct CptImage {
-    std::vector<unsigned char> img;
-    std::vector<int64_t> off;           // [T+1]
-    std::vector<int32_t> stage_start;   // [n_stages+1]
-    int32_t rows = 256;
-    int32_t feat_lds = 1;
-    int64_t max_stage_bytes = 0;
-  } cpt[2];
-  std::vector<int32_t> h_cpt_nint, h_cpt_depth, h_cpt_root;
   // binned heap layout (3): one image per input dtype (the ranks differ:
   // float32 view round_down_f32(t), float64 view t)
   struct BinImage {
     std::vector<unsigned char> img;   // [T][stride]
-    std::vector<unsigned char> tbl;   // [F][2^L] XT Eytzinger tables
+    std::vector<unsigned char> tbl;   // [F][2^L] XT Eytzinger tables, or 5-ary (kary > 0)
     int32_t L = 0;
+    int32_t kary = 0;                 // > 0: tbl holds float32 5-ary tables of this height
     int32_t b16 = 1;
     int32_t rows = 256;
     int32_t words = 0;                // packed bin words per row
     int64_t stride = 0;
+    uint32_t mask = ti::kBNodeOffMask;   // bin-offset bits of a node word
   } bh[2];
-  // binned explicit layout (4): explicit nodes whose threshold is a rank
-  struct BinExplicit {
-    std::vector<ExpNode> nodes;
-    std::vector<unsigned char> tbl;
-    int32_t L = 0;
-    int32_t b16 = 1;
-    int32_t rows = 256;
-    int32_t words = 0;
-    std::vector<unsigned char> sx;   // staged slot image (layout 5): [T][sx_slots] x 8 B
-  } bx[2];
-  // staged binned explicit (layout 5): slots per tree record (even, so records
-  // stay 16-byte aligned), the slot of every descriptor node, per-slot leaf
-  // values (ACC) and leaf ids
-  int64_t sx_slots = 0;
-  std::vector<int32_t> h_sx_slot;
-  std::vector<unsigned char> h_sx_vals;
-  std::vector<int32_t> h_sx_ids;
-  int32_t bx_ilp = 4;               // trees per lane in lockstep (4 or 8)
   // record explicit layout (6): 8-byte slots per input dtype (ranks differ),
   // shared per-tree first slot, per-slot leaf values / ids
   struct RecExplicit {
@@ -583,10 +549,8 @@ void free_device(DeviceForest& d) {
   (void)hipSetDevice(d.device);
   void* ptrs[] = {d.heap32, d.heap64, d.heap_leaf_ids, d.nodes, d.thr64, d.node_base, d.root,
                   d.leaf_base, d.leaves, d.exp_leaf_ids, d.tree_group, d.x_buf, d.out_buf,
-                  d.cpt_img[0], d.cpt_img[1], d.cpt_off[0], d.cpt_off[1], d.cpt_stage[0],
-                  d.cpt_stage[1], d.cpt_nint, d.cpt_depth, d.cpt_root, d.cat_words,
-                  d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1],
-                  d.bx_nodes[0], d.bx_nodes[1], d.bx_tbl[0], d.bx_tbl[1],
+                  d.cat_words, d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1],
+                  d.bx_tbl[0], d.bx_tbl[1],
                   d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias,
                   d.rx_recs[0], d.rx_recs[1], d.rx_base, d.rx_nint, d.lx_stage,
                   d.hx_top[0], d.hx_top[1]};
@@ -613,17 +577,8 @@ void free_device(DeviceForest& d) {
   d.thr64 = nullptr;
   d.node_base = d.leaf_base = nullptr;
   d.leaves = d.x_buf = d.out_buf = nullptr;
-  for (int i = 0; i < 2; ++i) {
-    d.cpt_img[i] = nullptr;
-    d.cpt_off[i] = nullptr;
-    d.cpt_stage[i] = nullptr;
-  }
-  d.cpt_nint = d.cpt_depth = d.cpt_root = nullptr;
   d.cat_words = nullptr;
-  for (int i = 0; i < 2; ++i) {
-    d.bh_img[i] = d.bh_tbl[i] = d.bx_tbl[i] = nullptr;
-    d.bx_nodes[i] = nullptr;
-  }
+  for (int i = 0; i < 2; ++i) d.bh_img[i] = d.bh_tbl[i] = d.bx_tbl[i] = nullptr;
   d.rx_recs[0] = d.rx_recs[1] = nullptr;
   d.rx_base = d.rx_nint = nullptr;
   d.lx_stage = nullptr;
@@ -831,115 +786,6 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
   if (!leaves.empty()) std::memcpy(f->h_leaves.data(), leaves.data(), f->h_leaves.size());
 }
 
-// ---------------------------------------------------------- compact packing
-// Trees with <= 512 internal nodes and <= 512 leaves, numbered breadth-first
-// like pack_explicit (so leaf ids / leaf_base are shared with it).  Returns
-// false when some tree does not fit the 10-bit child codes.
-constexpr int kCptMaxNodes = 512;
-
-bool compact_fits(const ti_forest_desc* d) {
-  if (d->n_features > 1024) return false;
-  for (int t = 0; t < d->n_trees; ++t) {
-    const int64_t b = d->tree_offset[t], e = d->tree_offset[t + 1];
-    int64_t n_int = 0;
-    for (int64_t g = b; g < e; ++g) n_int += d->feature[g] >= 0;
-    if (n_int > kCptMaxNodes || (e - b) - n_int > kCptMaxNodes) return false;
-  }
-  return true;
-}
-
-template <typename XT, typename ACC>
-void pack_compact(const ti_forest_desc* d, std::vector<unsigned char>* img, std::vector<int64_t>* off,
-                  std::vector<int32_t>* nint, std::vector<int32_t>* root) {
-  using Node = HeapNode<XT>;
-  const int LW = d->leaf_width;
-  off->assign(d->n_trees + 1, 0);
-  nint->assign(d->n_trees, 0);
-  root->assign(d->n_trees, 0);
-  img->clear();
-  std::vector<int32_t> queue, code;
-  for (int t = 0; t < d->n_trees; ++t) {
-    const int64_t b = d->tree_offset[t];
-    const int32_t n = static_cast<int32_t>(d->tree_offset[t + 1] - b);
-    code.assign(n, 0);
-    queue.assign(1, 0);
-    int32_t n_int = 0, n_leaf = 0;
-    for (size_t qi = 0; qi < queue.size(); ++qi) {
-      const int32_t v = queue[qi];
-      const int64_t g = b + v;
-      if (d->feature[g] < 0) {
-        code[v] = static_cast<int32_t>(ti::kCptLeaf) + n_leaf++;
-      } else {
-        code[v] = n_int++;
-        queue.push_back(d->left[g]);
-        queue.push_back(d->right[g]);
-      }
-    }
-    const size_t rec = align16(sizeof(Node) * n_int + sizeof(ACC) * n_leaf * LW);
-    const size_t base = img->size();
-    img->resize(base + rec, 0);
-    Node* nodes = reinterpret_cast<Node*>(img->data() + base);
-    ACC* leaves = reinterpret_cast<ACC*>(img->data() + base + sizeof(Node) * n_int);
-    for (size_t qi = 0; qi < queue.size(); ++qi) {
-      const int32_t v = queue[qi];
-      const int64_t g = b + v;
-      if (d->feature[g] < 0) {
-        const int32_t j = code[v] - static_cast<int32_t>(ti::kCptLeaf);
-        for (int k = 0; k < LW; ++k) leaves[j * LW + k] = static_cast<ACC>(d->leaf_value[g * LW + k]);
-        continue;
-      }
-      Node nd{};
-      nd.thr = sizeof(XT) == 4 ? static_cast<decltype(nd.thr)>(round_down_f32(d->threshold[g]))
-                               : static_cast<decltype(nd.thr)>(d->threshold[g]);
-      uint32_t w = static_cast<uint32_t>(d->feature[g]) |
-                   (static_cast<uint32_t>(code[d->left[g]]) << 10) |
-                   (static_cast<uint32_t>(code[d->right[g]]) << 20);
-      if (d->flags[g] & TI_NODE_ZERO_FLIP) w |= ti::kMetaZeroFlip;
-      if (d->flags[g] & TI_NODE_NAN_LEFT) w |= ti::kMetaNanLeft;
-      nd.meta = w;
-      nodes[code[v]] = nd;
-    }
-    (*nint)[t] = n_int;
-    (*root)[t] = code[0];
-    (*off)[t + 1] = static_cast<int64_t>(img->size());
-  }
-}
-
-// Feature mode, rows per tile and LDS stages of one compact image.  Returns
-// false if a single tree record cannot be staged.
-bool plan_compact(ti_forest* f, int idx, size_t xs) {
-  ti_forest::CptImage& ci = f->cpt[idx];
-  const int mode = env_int("TI_CPT_FEAT_LDS", -1);   // -1 auto, 0 HBM rows, 1 LDS image
-  const bool lds = mode >= 0 ? mode == 1
-                             : static_cast<size_t>(f->F) * 256 * xs <= static_cast<size_t>(40 * 1024);
-  ci.feat_lds = lds ? 1 : 0;
-  ci.rows = lds ? pick_rows(f->F, xs, 0) : 256;
-  if (ci.rows == 0) {
-    ci.feat_lds = 0;
-    ci.rows = 256;
-  }
-  const size_t fixed = (ci.feat_lds ? align16(static_cast<size_t>(f->F) * ci.rows * xs) : 0) + 16;
-  int64_t max_rec = 0;
-  for (int t = 0; t < f->T; ++t) max_rec = std::max(max_rec, ci.off[t + 1] - ci.off[t]);
-  const int64_t pf_cap = static_cast<int64_t>(ti::kPf) * 16 * ci.rows;
-  const int64_t min_stage = max_rec * std::min<int64_t>(ti::kTilp, f->T);
-  size_t n_wg = kLdsPerCu / (fixed + static_cast<size_t>(std::min(min_stage, pf_cap)));
-  if (n_wg < 1) n_wg = 1;
-  int64_t budget = static_cast<int64_t>(kLdsPerCu / n_wg) - static_cast<int64_t>(fixed);
-  budget = std::min(budget, pf_cap);
-  if (budget < max_rec) return false;
-  ci.stage_start.assign(1, 0);
-  ci.max_stage_bytes = 0;
-  int t0 = 0;
-  while (t0 < f->T) {
-    int t1 = t0 + 1;
-    while (t1 < f->T && ci.off[t1 + 1] - ci.off[t0] <= budget) ++t1;
-    ci.stage_start.push_back(t1);
-    ci.max_stage_bytes = std::max(ci.max_stage_bytes, ci.off[t1] - ci.off[t0]);
-    t0 = t1;
-  }
-  return true;
-}
 
 // ------------------------------------------------------ binned heap packing
 // Rank binning (treeinfer_kernels.h, stage_bins): per feature the sorted
@@ -1081,7 +927,18 @@ bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
   if (static_cast<int64_t>(bi->words) * R * 4 > static_cast<int64_t>(ti::kBNodeOffMask) + 1) return false;
   bi->rows = R;
   bi->L = rt.L;
-  eytzinger_tables(rt, &bi->tbl);
+  bi->kary = 0;
+  if constexpr (sizeof(XT) == 4) {
+    if (env_int("TI_KARY", 1) != 0) kary_tables(rt, &bi->tbl, &bi->kary);
+    else eytzinger_tables(rt, &bi->tbl);
+  } else {
+    eytzinger_tables(rt, &bi->tbl);
+  }
+  // 512-row tiles: the offset bits are 0, 1 and 11..14, and each node word
+  // also carries its own heap index in bits 3..10 (the fixed-layout walk's
+  // pair address; treeinfer_kernels.h, kBNodeOffMask512)
+  const bool with_index = R == 512;
+  bi->mask = with_index ? ti::kBNodeOffMask512 : ti::kBNodeOffMask;
   auto node_word = [&](int64_t g) -> uint32_t {
     const int f = d->feature[g];
     const uint32_t rank = rt.rank(f, d->threshold[g]);
@@ -1113,123 +970,15 @@ bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
         if (leaf_ids) (*leaf_ids)[static_cast<size_t>(t) * NE + slot] = d->leaf_id[g];
         continue;
       }
+      const uint32_t idx = with_index ? static_cast<uint32_t>(it.heap) << 3 : 0u;
       if (d->feature[g] < 0) {   // shallow leaf: always-left padding down to level D
-        nodes[it.heap] = 0xFFFFu << 16;
+        nodes[it.heap] = (0xFFFFu << 16) | idx;
         st.push_back(Item{it.node, 2 * it.heap, it.level + 1});
         st.push_back(Item{it.node, 2 * it.heap + 1, it.level + 1});
       } else {
-        nodes[it.heap] = node_word(g);
+        nodes[it.heap] = node_word(g) | idx;
         st.push_back(Item{d->left[g], 2 * it.heap, it.level + 1});
         st.push_back(Item{d->right[g], 2 * it.heap + 1, it.level + 1});
-      }
-    }
-  }
-  return true;
-}
-
-// Slots of the staged explicit layout (see kSxLeaf): breadth-first, the root in
-// slot 0 and the children of each internal node in the next two free slots.
-// Leaves back per-slot value / id tables.  Leaves f->sx_slots = 0 when a tree
-// has more than kSxMaxSlots nodes (its record would not leave room in LDS).
-constexpr int64_t kSxMaxSlots = 1024;
-void plan_slots(const ti_forest_desc* d, ti_forest* f) {
-  f->sx_slots = 0;
-  int64_t ns = 0;
-  for (int t = 0; t < d->n_trees; ++t) ns = std::max(ns, d->tree_offset[t + 1] - d->tree_offset[t]);
-  ns = (ns + 1) & ~int64_t(1);
-  if (ns > kSxMaxSlots) return;
-  const int LW = d->leaf_width;
-  const size_t as = f->accum == TI_F64 ? 8 : 4;
-  f->h_sx_slot.assign(d->n_nodes, 0);
-  f->h_sx_vals.assign(static_cast<size_t>(d->n_trees) * ns * LW * as, 0);
-  f->h_sx_ids.assign(static_cast<size_t>(d->n_trees) * ns, 0);
-  std::vector<int32_t> q;
-  for (int t = 0; t < d->n_trees; ++t) {
-    const int64_t b = d->tree_offset[t];
-    q.assign(1, 0);
-    int32_t next = 1;
-    for (size_t qi = 0; qi < q.size(); ++qi) {
-      const int64_t g = b + q[qi];
-      if (d->feature[g] < 0) continue;
-      f->h_sx_slot[b + d->left[g]] = next;
-      f->h_sx_slot[b + d->right[g]] = next + 1;
-      next += 2;
-      q.push_back(d->left[g]);
-      q.push_back(d->right[g]);
-    }
-    for (int64_t g = b; g < d->tree_offset[t + 1]; ++g) {
-      if (d->feature[g] >= 0) continue;
-      const size_t s = static_cast<size_t>(t) * ns + f->h_sx_slot[g];
-      f->h_sx_ids[s] = d->leaf_id[g];
-      for (int k = 0; k < LW; ++k) {
-        const double v = d->leaf_value[g * LW + k];
-        if (as == 8) {
-          std::memcpy(&f->h_sx_vals[(s * LW + k) * 8], &v, 8);
-        } else {
-          const float v32 = static_cast<float>(v);
-          std::memcpy(&f->h_sx_vals[(s * LW + k) * 4], &v32, 4);
-        }
-      }
-    }
-  }
-  f->sx_slots = ns;
-}
-
-// Rank-coded copy of the explicit nodes (pack_explicit must have run), and of
-// the staged slots when plan_slots accepted the trees.  Returns false when a
-// feature has more than 65,533 distinct thresholds or the bin image does not
-// fit 64 KB even at 64-row tiles.
-template <typename XT>
-bool pack_bexplicit(const ti_forest_desc* d, ti_forest* f, ti_forest::BinExplicit* bx) {
-  const RankTables<XT> rt = collect_ranks<XT>(d, f->zero_rule != 0);
-  if (rt.m_max > 65533) return false;
-  bx->b16 = rt.m_max > 253 ? 1 : 0;
-  const int P = bx->b16 ? 2 : 4;
-  bx->words = (d->n_features + P - 1) / P;
-  int R = 64;   // a power of two in [64, 512], as pack_rexplicit
-  while (R < 512 && 2 * R <= env_int("TI_BEXP_ROWS", 256)) R *= 2;
-  while (R > 64 && static_cast<size_t>(bx->words) * R * 4 > kFeatLdsMax) R >>= 1;
-  if (static_cast<size_t>(bx->words) * R * 4 > kFeatLdsMax) return false;
-  bx->rows = R;
-  bx->L = rt.L;
-  eytzinger_tables(rt, &bx->tbl);
-  bx->nodes.resize(f->h_nodes.size());
-  for (size_t i = 0; i < f->h_nodes.size(); ++i) {
-    const int64_t g = f->h_exp_src[i];
-    const int fe = d->feature[g];
-    ExpNode e = f->h_nodes[i];
-    const bool zflip = (d->flags[g] & TI_NODE_ZERO_FLIP) != 0;
-    const uint32_t w = rt.rank(fe, d->threshold[g]) | ((zflip ? rt.zbin[fe] : 0u) << 16);
-    std::memcpy(&e.thr, &w, sizeof(w));
-    e.meta = static_cast<uint32_t>((fe / P) * R * 4 + (fe % P) * (4 / P));
-    if (d->flags[g] & TI_NODE_NAN_LEFT) e.meta |= ti::kMetaNanLeft;
-    if (zflip) e.meta |= ti::kMetaZeroFlip;
-    bx->nodes[i] = e;
-  }
-  bx->sx.clear();
-  if (f->sx_slots > 0) {   // the same nodes as staged slots (layout 5)
-    const int64_t ns = f->sx_slots;
-    bx->sx.assign(static_cast<size_t>(d->n_trees) * ns * 8, 0);
-    for (int t = 0; t < d->n_trees; ++t) {
-      const int64_t b = d->tree_offset[t];
-      const int64_t n = d->tree_offset[t + 1] - b;
-      for (int64_t s = 0; s < ns; ++s) {   // every slot a self-loop leaf until filled
-        const uint32_t rec[2] = {ti::kSxLeaf, ti::kSxNanLeft | static_cast<uint32_t>(s)};
-        std::memcpy(&bx->sx[(t * ns + s) * 8], rec, 8);
-      }
-      for (int64_t v = 0; v < n; ++v) {
-        const int64_t g = b + v;
-        const int fe = d->feature[g];
-        if (fe < 0) continue;
-        const bool zflip = (d->flags[g] & TI_NODE_ZERO_FLIP) != 0;
-        const uint32_t off = static_cast<uint32_t>((fe / P) * R * 4 + (fe % P) * (4 / P));
-        if (off > 0xFFFFu) return false;
-        uint32_t rec[2];
-        rec[0] = (rt.rank(fe, d->threshold[g]) << 16) | off;
-        rec[1] = ((zflip ? rt.zbin[fe] : 0u) << 16) |
-                 ((d->flags[g] & TI_NODE_NAN_LEFT) ? ti::kSxNanLeft : 0u) |
-                 static_cast<uint32_t>(f->h_sx_slot[b + d->left[g]]);
-        std::memcpy(&bx->sx[(t * ns + f->h_sx_slot[g]) * 8], rec, 8);
       }
     }
   }
@@ -1728,18 +1477,6 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
     if ((rc = upload(&d.heap32, f->h_heap32, &d.bytes))) return rc;
     if ((rc = upload(&d.heap64, f->h_heap64, &d.bytes))) return rc;
     if ((rc = upload(&d.heap_leaf_ids, f->h_heap_leaf_ids, &d.bytes))) return rc;
-  } else if (f->layout == 4) {
-    for (int i = 0; i < 2; ++i) {
-      if ((rc = upload(&d.bx_nodes[i], f->bx[i].nodes, &d.bytes))) return rc;
-      if ((rc = upload(&d.bx_tbl[i], f->bx[i].tbl, &d.bytes))) return rc;
-    }
-    if ((rc = upload(&d.node_base, f->h_node_base, &d.bytes))) return rc;
-    if ((rc = upload(&d.root, f->h_root, &d.bytes))) return rc;
-    if ((rc = upload(&d.leaf_base, f->h_leaf_base, &d.bytes))) return rc;
-    unsigned char* lv = nullptr;
-    if ((rc = upload(&lv, f->h_leaves, &d.bytes))) return rc;
-    d.leaves = lv;
-    if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
   } else if (f->layout == 6 || f->layout == 7 || f->layout == 8) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.rx_recs[i], f->rx[i].recs, &d.bytes))) return rc;
@@ -1771,32 +1508,12 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
       d.leaves = lv;
     }
     if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
-  } else if (f->layout == 5) {
-    for (int i = 0; i < 2; ++i) {
-      if ((rc = upload(&d.bh_img[i], f->bx[i].sx, &d.bytes))) return rc;
-      if ((rc = upload(&d.bx_tbl[i], f->bx[i].tbl, &d.bytes))) return rc;
-    }
-    unsigned char* lv = nullptr;
-    if ((rc = upload(&lv, f->h_sx_vals, &d.bytes))) return rc;
-    d.leaves = lv;
-    if ((rc = upload(&d.exp_leaf_ids, f->h_sx_ids, &d.bytes))) return rc;
   } else if (f->layout == 3) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.bh_img[i], f->bh[i].img, &d.bytes))) return rc;
       if ((rc = upload(&d.bh_tbl[i], f->bh[i].tbl, &d.bytes))) return rc;
     }
     if ((rc = upload(&d.heap_leaf_ids, f->h_heap_leaf_ids, &d.bytes))) return rc;
-  } else if (f->layout == 2) {
-    for (int i = 0; i < 2; ++i) {
-      if ((rc = upload(&d.cpt_img[i], f->cpt[i].img, &d.bytes))) return rc;
-      if ((rc = upload(&d.cpt_off[i], f->cpt[i].off, &d.bytes))) return rc;
-      if ((rc = upload(&d.cpt_stage[i], f->cpt[i].stage_start, &d.bytes))) return rc;
-    }
-    if ((rc = upload(&d.cpt_nint, f->h_cpt_nint, &d.bytes))) return rc;
-    if ((rc = upload(&d.cpt_depth, f->h_cpt_depth, &d.bytes))) return rc;
-    if ((rc = upload(&d.cpt_root, f->h_cpt_root, &d.bytes))) return rc;
-    if ((rc = upload(&d.leaf_base, f->h_leaf_base, &d.bytes))) return rc;
-    if ((rc = upload(&d.exp_leaf_ids, f->h_exp_leaf_ids, &d.bytes))) return rc;
   } else {
     if ((rc = upload(&d.nodes, f->h_nodes, &d.bytes))) return rc;
     if ((rc = upload(&d.thr64, f->h_thr64, &d.bytes))) return rc;
@@ -1829,13 +1546,6 @@ KernelFn select_bheap(int xdt, int accum, int K, bool b16, int pf) {
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(3, K, true, false, b16, pf);
   if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(3, K, true, false, b16, pf);
   return ti::kernels_df(3, K, true, false, b16, pf);
-}
-
-KernelFn select_bexplicit(int xdt, int accum, int K, bool b16, bool z, int ilp) {
-  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(4, K, true, z, b16, ilp);
-  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(4, K, true, z, b16, ilp);
-  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(4, K, true, z, b16, ilp);
-  return ti::kernels_df(4, K, true, z, b16, ilp);
 }
 
 KernelFn select_rexplicit(int xdt, int accum, int K, bool z, int ilp) {
@@ -1879,13 +1589,6 @@ KernelFn select_hexplicit(int xdt, int accum, int K, bool z, int ilp) {
   return ti::kernels_df(8, K, true, z, true, ilp);
 }
 
-KernelFn select_sexplicit(int xdt, int accum, int K, bool b16, bool z, int ilp) {
-  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(5, K, true, z, b16, ilp);
-  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(5, K, true, z, b16, ilp);
-  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(5, K, true, z, b16, ilp);
-  return ti::kernels_df(5, K, true, z, b16, ilp);
-}
-
 std::mutex g_attr_mu;
 std::set<std::pair<int, const void*>> g_attr_done;
 
@@ -1921,6 +1624,20 @@ int output_dtype(const ti_forest* f, int kind) {
 
 size_t dtype_size(int dt) { return dt == TI_F64 ? 8 : 4; }
 
+// Whether a binned-heap launch takes the fixed-layout walk (bheap_fix_kernel):
+// float32 input and sums, one scalar leaf per leaf, depth-8 records of 2 KB,
+// 512-row tiles (the node words carry their heap index) and at most 14 bin
+// words (the image ends below kFixFlag); leaf ids keep the indexed walk.
+// TI_BHEAP_FIX=0 turns it off.
+bool bheap_fixed(const ti_forest* f, int xdt, int kind) {
+  if (f->layout != 3 || xdt != TI_F32 || f->accum != TI_F32 || f->LW != 1 || f->depth != 8)
+    return false;
+  if (kind != TI_OUTPUT_MARGIN && kind != TI_OUTPUT_PREDICT) return false;
+  const ti_forest::BinImage& bi = f->bh[0];
+  return env_int("TI_BHEAP_FIX", 1) != 0 && bi.rows == ti::kFixRows && bi.mask == ti::kBNodeOffMask512 &&
+         bi.stride == ti::kFixTree && static_cast<uint32_t>(bi.words) * 2048u <= ti::kFixFlag;
+}
+
 int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, int32_t cols,
            int64_t stride, int kind, void* out, hipStream_t stream) {
   if (rows <= 0) return TI_OK;
@@ -1930,13 +1647,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   int R;
   if (f->layout == 0) {
     R = xdt == TI_F64 ? f->rows64 : f->rows32;
-  } else if (f->layout == 2) {
-    const ti_forest::CptImage& ci = f->cpt[xdt == TI_F64 ? 1 : 0];
-    R = ci.feat_lds ? ci.rows : 0;
   } else if (f->layout == 3) {
     R = f->bh[xdt == TI_F64 ? 1 : 0].rows;
-  } else if (f->layout == 4 || f->layout == 5) {
-    R = f->bx[xdt == TI_F64 ? 1 : 0].rows;
   } else if (f->layout >= 6 && f->layout <= 9) {
     R = f->rx[xdt == TI_F64 ? 1 : 0].rows;
   } else {
@@ -1948,8 +1660,6 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   if (!feat_lds) R = 256;
   size_t feat_bytes = feat_lds ? align16(static_cast<size_t>(f->F) * R * xs) : 0;
   if (f->layout == 3) feat_bytes = static_cast<size_t>(f->bh[xdt == TI_F64 ? 1 : 0].words) * R * 4;
-  if (f->layout == 4 || f->layout == 5)
-    feat_bytes = static_cast<size_t>(f->bx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
   if (f->layout >= 6 && f->layout <= 9)
     feat_bytes = static_cast<size_t>(f->rx[xdt == TI_F64 ? 1 : 0].words) * R * 4;
 
@@ -2030,6 +1740,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     S = std::min<int64_t>(S, f->T);
     const int pf = S * stride_b <= static_cast<int64_t>(4) * 16 * R ? 4 : 8;
     a.X = X;
+    a.bin_mask = bi.mask;
+    a.bin_kary = bi.kary;
     a.trees = d.bh_img[ii];
     a.tree_stride = stride_b;
     a.heap_leaf_ids = d.heap_leaf_ids;
@@ -2044,27 +1756,17 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
                                                         static_cast<size_t>(f->F + 7) & ~size_t(7)));
     lds = fixed + ar;
     KernelFn fn = select_bheap(xdt, f->accum, f->K, bi.b16 != 0, pf);
-    int rc = ensure_lds_attr(d.device, fn);
-    if (rc) return rc;
-    const int64_t grid = (rows + R - 1) / R;
-    if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
-    TI_HIP(hipGetLastError());
-    return TI_OK;
-  } else if (f->layout == 4) {
-    const int ii = xdt == TI_F64 ? 1 : 0;
-    const ti_forest::BinExplicit& bx = f->bx[ii];
-    a.nodes = d.bx_nodes[ii];
-    a.node_base = d.node_base;
-    a.root = d.root;
-    a.leaf_base = d.leaf_base;
-    a.leaves = d.leaves;
-    a.exp_leaf_ids = d.exp_leaf_ids;
-    a.bin_tbl = d.bx_tbl[ii];
-    a.bin_L = bx.L;
-    a.bin_words = bx.words;
-    lds = feat_bytes + 16;
-    KernelFn fn = select_bexplicit(xdt, f->accum, f->K, bx.b16 != 0, f->zero_rule != 0, f->bx_ilp);
+    if (bheap_fixed(f, xdt, kind)) {
+      // fixed layout (bheap_fix_kernel): [bins][flag][NG groups of 4 trees at
+      // kFixStage]; the binning goes through the stage area, 4 NG columns at a
+      // time.  NG = 1: 38,912 B, 4 workgroups (32 waves) per CU
+      const int ng = std::min(2, std::max(1, env_int("TI_BHEAP_NG", 1)));
+      fn = ti::kernels_ff(10, f->K, true, false, bi.b16 != 0, ng);
+      a.stage_trees = 4 * ng;
+      a.bin_chunk = 4 * ng;
+      a.stage_off = static_cast<int32_t>(ti::kFixStage);
+      lds = ti::kFixStage + static_cast<size_t>(4 * ng) * ti::kFixTree;
+    }
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -2184,53 +1886,6 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
-  } else if (f->layout == 5) {
-    // stage: S trees, as many as the prefetch registers carry (8 x 16 B per
-    // thread), at least one
-    const int ii = xdt == TI_F64 ? 1 : 0;
-    const ti_forest::BinExplicit& bx = f->bx[ii];
-    const int64_t stride_b = f->sx_slots * 8;
-    if (R > 256 || stride_b > static_cast<int64_t>(8) * 16 * R)
-      return fail(TI_ERR_UNSUPPORTED, "staged explicit layout needs <= 256-row tiles");
-    int64_t S = static_cast<int64_t>(8) * 16 * R / stride_b;
-    static const int force_s = env_int("TI_SX_STAGE", 0);
-    if (force_s > 0) S = std::min<int64_t>(force_s, S);
-    S = std::min<int64_t>(S, f->T);
-    a.trees = d.bh_img[ii];
-    a.tree_stride = stride_b;
-    a.stage_trees = static_cast<int32_t>(S);
-    a.leaves = d.leaves;
-    a.exp_leaf_ids = d.exp_leaf_ids;
-    a.bin_tbl = d.bx_tbl[ii];
-    a.bin_L = bx.L;
-    a.bin_words = bx.words;
-    a.stage_off = static_cast<int32_t>(align16(feat_bytes + 4));
-    lds = static_cast<size_t>(a.stage_off) + static_cast<size_t>(S * stride_b);
-    if (lds > kLdsPerCu) return fail(TI_ERR_UNSUPPORTED, "staged explicit layout exceeds LDS");
-    KernelFn fn = select_sexplicit(xdt, f->accum, f->K, bx.b16 != 0, f->zero_rule != 0, f->bx_ilp);
-    int rc = ensure_lds_attr(d.device, fn);
-    if (rc) return rc;
-    const int64_t grid = (rows + R - 1) / R;
-    if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
-    TI_HIP(hipGetLastError());
-    return TI_OK;
-  } else if (f->layout == 2) {
-    const int ii = xdt == TI_F64 ? 1 : 0;
-    const ti_forest::CptImage& ci = f->cpt[ii];
-    a.trees = d.cpt_img[ii];
-    a.cpt_off = d.cpt_off[ii];
-    a.stage_start = d.cpt_stage[ii];
-    a.n_stages = static_cast<int32_t>(ci.stage_start.size() - 1);
-    a.cpt_nint = d.cpt_nint;
-    a.cpt_depth = d.cpt_depth;
-    a.cpt_root = d.cpt_root;
-    a.leaf_base = d.leaf_base;
-    a.exp_leaf_ids = d.exp_leaf_ids;
-    int sh = 0;
-    while ((static_cast<size_t>(1) << sh) < static_cast<size_t>(R) * xs) ++sh;
-    a.feat_shift = sh;
-    lds = feat_bytes + 16 + static_cast<size_t>(ci.max_stage_bytes);
   } else {
     a.nodes = d.nodes;
     a.thr64 = d.thr64;
@@ -2316,6 +1971,16 @@ int predict_pipelined(ti_forest* f, int slot, DeviceForest& d, const unsigned ch
   const size_t x_row = static_cast<size_t>(stride) * xs;
   const size_t x_cap = static_cast<size_t>(ch) * x_row;
   const size_t o_cap = static_cast<size_t>(ch) * os;
+  // Whatever path leaves this function (an early TI_HIP return or a failed
+  // launch included), no copy or kernel queued on a lane outlives it: the
+  // next call reuses -- or frees -- the lane buffers that work reads and writes.
+  struct LaneSync {
+    DeviceForest& d;
+    ~LaneSync() {
+      for (int l = 0; l < 2; ++l)
+        if (d.lane_stream[l]) (void)hipStreamSynchronize(d.lane_stream[l]);
+    }
+  } lane_sync{d};
   if (d.lane_x_cap < x_cap || d.lane_o_cap < o_cap) {
     for (int l = 0; l < 2; ++l) {
       if (d.lane_hx[l]) (void)hipHostFree(d.lane_hx[l]);
@@ -2843,41 +2508,23 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
 
   const size_t acc_sz = f->accum == TI_F64 ? 8 : 4;
   const int D = f->depth;
-  // layout: heap for depth <= 8, compact (LDS-staged) for small irregular
-  // trees, explicit (nodes in HBM) otherwise; TI_FORCE_LAYOUT=heap|compact|
-  // explicit overrides (tests run every layout on the same forest)
+  // layout: binned heap for depth <= 8, the record layouts (6-9) for deeper
+  // trees, the float explicit kernel for categorical splits;
+  // TI_FORCE_LAYOUT=heap|explicit|rexplicit|lexplicit|hexplicit|texplicit
+  // overrides (tests run every layout on the same forest)
   const char* force = std::getenv("TI_FORCE_LAYOUT");
   std::string want = force ? force : "";
   bool use_heap = D <= kMaxHeapDepth;
-  // compact layout: LDS-staged irregular trees (F = 100: explicit 19.1 ms,
-  // compact 29.6 ms with the feature image in LDS, 160 ms reading rows from HBM)
-  // (measured on 1000 x 255-leaf LightGBM forests: explicit 7.8 ms vs compact
-  // 8.8 ms at F = 28, so compact is opt-in only until it beats explicit)
-  bool use_compact = false;
-  if (want == "heap" && D <= kMaxHeapDepth) { use_heap = true; use_compact = false; }
-  if (want == "compact" && compact_fits(desc)) { use_heap = false; use_compact = true; }
-  if (want == "explicit" || want == "bexplicit" || want == "sexplicit" || want == "rexplicit" ||
-      want == "lexplicit" || want == "hexplicit" || want == "texplicit") {
+  if (want == "heap" && D <= kMaxHeapDepth) use_heap = true;
+  if (want == "explicit" || want == "rexplicit" || want == "lexplicit" || want == "hexplicit" ||
+      want == "texplicit")
     use_heap = false;
-    use_compact = false;
-  }
   // categorical splits are evaluated by the explicit kernel only
-  if (f->has_cat) { use_heap = false; use_compact = false; }
-  if (use_compact) {
-    f->h_cpt_depth.assign(depth.begin(), depth.end());
-    if (f->accum == TI_F64) {
-      pack_compact<float, double>(desc, &f->cpt[0].img, &f->cpt[0].off, &f->h_cpt_nint, &f->h_cpt_root);
-      pack_compact<double, double>(desc, &f->cpt[1].img, &f->cpt[1].off, &f->h_cpt_nint, &f->h_cpt_root);
-    } else {
-      pack_compact<float, float>(desc, &f->cpt[0].img, &f->cpt[0].off, &f->h_cpt_nint, &f->h_cpt_root);
-      pack_compact<double, float>(desc, &f->cpt[1].img, &f->cpt[1].off, &f->h_cpt_nint, &f->h_cpt_root);
-    }
-    if (!plan_compact(f.get(), 0, 4) || !plan_compact(f.get(), 1, 8)) use_compact = false;
-  }
+  if (f->has_cat) use_heap = false;
   // binned heap (rank-binned features, 4-byte nodes) for complete-able trees
   // without LightGBM zero-missing or categorical splits; TI_FORCE_LAYOUT=heap
   // keeps the float-compare heap kernel
-  bool use_bheap = use_heap && !use_compact && want != "heap" && f->zero_rule == 0 && D >= 1 &&
+  bool use_bheap = use_heap && want != "heap" && f->zero_rule == 0 && D >= 1 &&
                    env_int("TI_NO_BHEAP", 0) == 0;
   if (use_bheap) {
     bool ok;
@@ -2894,9 +2541,6 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   }
   if (use_bheap) {
     f->layout = 3;
-  } else if (use_compact) {
-    f->layout = 2;
-    pack_explicit<char>(desc, f.get(), /*leaf_ids_only=*/true);
   } else if (use_heap) {
     const int NI = (1 << D) - 1, NL = 1 << D;
     f->layout = 0;
@@ -2926,7 +2570,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
     // record explicit slots (layout 6) unless a categorical split needs raw
     // values or another explicit kernel is forced
     bool rx_ok = false;
-    if (!f->has_cat && want != "explicit" && want != "bexplicit" && want != "sexplicit" &&
+    if (!f->has_cat && want != "explicit" &&
         env_int("TI_NO_REXPLICIT", 0) == 0) {
       std::vector<uint32_t> slot_of;
       rx_ok = plan_rx_slots(desc, f.get(), &slot_of);
@@ -2967,34 +2611,6 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         f->rx_slots = 0;
       }
     }
-    // rank-binned explicit nodes unless a categorical split needs raw values
-    // (TI_FORCE_LAYOUT=explicit keeps the float-compare kernel)
-    if (!rx_ok && !f->has_cat && want != "explicit" && env_int("TI_NO_BEXPLICIT", 0) == 0) {
-      // the LDS-staged walk (layout 5) is opt-in: at C3's F = 100 the stage costs
-      // the third workgroup per CU and the walk runs 0.65x layout 4
-      if (want == "sexplicit") plan_slots(desc, f.get());
-      if (pack_bexplicit<float>(desc, f.get(), &f->bx[0]) &&
-          pack_bexplicit<double>(desc, f.get(), &f->bx[1])) {
-        f->layout = 4;
-        // Tree ILP from the mean leaf depth: forests whose paths are short on
-        // average (leaf-wise, C3: mean leaf depth ~9) need 8 trees in flight
-        // to cover the L2 latency (measured 8.97 vs 10.8 ms at 4); deep
-        // balanced forests (sklearn depth 16, C4) are faster at 4 (3.46 vs
-        // 3.61 ms at 8), where a group's deepest path costs more.
-        const double mean_depth = mean_leaf_depth(desc);
-        f->bx_ilp = mean_depth < 12.0 ? 8 : 4;
-        const int force_ilp = env_int("TI_BEXP_ILP", 0);
-        if (force_ilp > 0) f->bx_ilp = force_ilp >= 8 ? 8 : 4;
-        // trees small enough to stage in LDS walk from the stage (layout 5)
-        if (f->sx_slots > 0 && !f->bx[0].sx.empty() && !f->bx[1].sx.empty()) {
-          f->layout = 5;
-          const int force_sx = env_int("TI_SX_ILP", 0);
-          f->bx_ilp = force_sx > 0 ? (force_sx >= 8 ? 8 : 4) : 8;
-        }
-      } else {
-        for (auto& bx : f->bx) bx = ti_forest::BinExplicit();
-      }
-    }
   }
   keep_shap_source(desc, f.get());
   for (int i = 0; i < n_devices; ++i) {
@@ -3013,21 +2629,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   f->h_thr64.clear(); f->h_thr64.shrink_to_fit();
   f->h_cat_words.clear(); f->h_cat_words.shrink_to_fit();
   f->h_leaves.clear(); f->h_leaves.shrink_to_fit();
-  for (auto& ci : f->cpt) {
-    ci.img.clear();
-    ci.img.shrink_to_fit();
-  }
-  f->h_sx_slot.clear(); f->h_sx_slot.shrink_to_fit();
-  f->h_sx_vals.clear(); f->h_sx_vals.shrink_to_fit();
-  f->h_sx_ids.clear(); f->h_sx_ids.shrink_to_fit();
-  for (auto& bx : f->bx) {
-    bx.sx.clear();
-    bx.sx.shrink_to_fit();
-    bx.nodes.clear();
-    bx.nodes.shrink_to_fit();
-    bx.tbl.clear();
-    bx.tbl.shrink_to_fit();
-  }
+
   f->h_exp_src.clear();
   f->h_exp_src.shrink_to_fit();
   for (auto& rx : f->rx) {
@@ -3073,6 +2675,8 @@ int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
     for (auto& p : f->parts) info->device_bytes += p->devs.empty() ? 0 : p->devs[0]->bytes;
   }
   info->tree_stride_bytes = f->layout == 0 ? f->stride32 : f->layout == 3 ? f->bh[0].stride : 0;
+  info->walk = bheap_fixed(f, TI_F32, TI_OUTPUT_PREDICT) ? 1 : 0;
+  info->bin_bits = f->layout == 3 ? (f->bh[0].b16 ? 16 : 8) : 0;
   return TI_OK;
 }
 

@@ -9,9 +9,10 @@ namespace ti {
 
 using KernelFn = void (*)(KArgs);
 
-// layout: 0 heap, 1 explicit, 2 compact, 3 binned heap, 4 binned explicit,
-// 5 staged binned explicit, 6 record explicit, 7 staged record explicit,
-// 8 heap top + record bottom, 9 heap top + staged record bottom.
+// layout: 0 heap, 1 explicit, 3 binned heap, 6 record explicit, 7 staged
+// record explicit, 8 heap top + record bottom, 9 heap top + staged record
+// bottom (2, 4 and 5 were retired in round 3); 10 selects the fixed-layout
+// walk of layout 3 (bheap_fix_kernel).
 // fl: feature image in
 // LDS; z: LightGBM zero rule; b16 / pf: binned heap bin width and prefetch
 // depth.
@@ -57,33 +58,12 @@ KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
     if (pf >= 8) return rexplicit_predict_kernel<XT, ACC, KMAX, false, 8>;
     return rexplicit_predict_kernel<XT, ACC, KMAX, false, 4>;
   }
-  if (layout == 5) {   // pf carries the tree ILP (4 or 8)
-    if constexpr (sizeof(ACC) == 8) {
-      if (z) {
-        if (pf >= 8) return b16 ? sexplicit_predict_kernel<XT, ACC, KMAX, true, true, 8>
-                                : sexplicit_predict_kernel<XT, ACC, KMAX, false, true, 8>;
-        return b16 ? sexplicit_predict_kernel<XT, ACC, KMAX, true, true, 4>
-                   : sexplicit_predict_kernel<XT, ACC, KMAX, false, true, 4>;
-      }
+  if (layout == 10) {   // binned heap, fixed layout: float X, float sums; pf carries NG
+    if constexpr (sizeof(XT) == 4 && sizeof(ACC) == 4) {
+      if (b16) return pf >= 2 ? bheap_fix_kernel<XT, KMAX, true, 2> : bheap_fix_kernel<XT, KMAX, true, 1>;
+      return pf >= 2 ? bheap_fix_kernel<XT, KMAX, false, 2> : bheap_fix_kernel<XT, KMAX, false, 1>;
     }
-    if (pf >= 8) return b16 ? sexplicit_predict_kernel<XT, ACC, KMAX, true, false, 8>
-                            : sexplicit_predict_kernel<XT, ACC, KMAX, false, false, 8>;
-    return b16 ? sexplicit_predict_kernel<XT, ACC, KMAX, true, false, 4>
-               : sexplicit_predict_kernel<XT, ACC, KMAX, false, false, 4>;
-  }
-  if (layout == 4) {   // pf carries the tree ILP (4 or 8)
-    if constexpr (sizeof(ACC) == 8) {
-      if (z) {
-        if (pf >= 8) return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, true, 8>
-                                : bexplicit_predict_kernel<XT, ACC, KMAX, false, true, 8>;
-        return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, true, 4>
-                   : bexplicit_predict_kernel<XT, ACC, KMAX, false, true, 4>;
-      }
-    }
-    if (pf >= 8) return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, false, 8>
-                            : bexplicit_predict_kernel<XT, ACC, KMAX, false, false, 8>;
-    return b16 ? bexplicit_predict_kernel<XT, ACC, KMAX, true, false, 4>
-               : bexplicit_predict_kernel<XT, ACC, KMAX, false, false, 4>;
+    return nullptr;
   }
   if (layout == 3) {
     if (b16) return pf <= 4 ? bheap_predict_kernel<XT, ACC, KMAX, true, 4>
@@ -96,16 +76,12 @@ KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
     if (z) {
       if (layout == 0) return fl ? heap_predict_kernel<XT, ACC, KMAX, true, true>
                                  : heap_predict_kernel<XT, ACC, KMAX, false, true>;
-      if (layout == 2) return fl ? compact_predict_kernel<XT, ACC, KMAX, true, true>
-                                 : compact_predict_kernel<XT, ACC, KMAX, false, true>;
       return fl ? explicit_predict_kernel<XT, ACC, KMAX, true, true>
                 : explicit_predict_kernel<XT, ACC, KMAX, false, true>;
     }
   }
   if (layout == 0) return fl ? heap_predict_kernel<XT, ACC, KMAX, true, false>
                              : heap_predict_kernel<XT, ACC, KMAX, false, false>;
-  if (layout == 2) return fl ? compact_predict_kernel<XT, ACC, KMAX, true, false>
-                             : compact_predict_kernel<XT, ACC, KMAX, false, false>;
   return fl ? explicit_predict_kernel<XT, ACC, KMAX, true, false>
             : explicit_predict_kernel<XT, ACC, KMAX, false, false>;
 }

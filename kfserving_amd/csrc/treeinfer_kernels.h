@@ -49,9 +49,6 @@
 #define TI_BIN_Q 8   // binned heap: features binary-searched at once per lane (the temp
                      // area holds 8 columns of a 512-row tile: more would cost LDS)
 #endif
-#ifndef TI_NT_X
-#define TI_NT_X 0   // binned staging: non-temporal (streaming) feature loads
-#endif
 
 namespace ti {
 
@@ -60,7 +57,6 @@ constexpr uint32_t kMetaZeroFlip = 0x40000000u;
 constexpr uint32_t kMetaCat = 0x20000000u;        // explicit layout: categorical node
 constexpr uint32_t kMetaFeatMask = 0x00FFFFFFu;
 constexpr int kMaxGroups = 16;
-constexpr uint32_t kCptLeaf = 512u;       // compact child code >= 512: leaf (code - 512)
 constexpr int kExpIlp = TI_EXP_ILP;       // trees per lane in the global explicit kernels
 constexpr int kTilp = TI_TILP;
 constexpr int kBTilp = TI_BTILP;
@@ -106,14 +102,9 @@ struct KArgs {
   const void* leaves;             // [n_leaves * leaf_width] ACC
   const int32_t* exp_leaf_ids;    // [n_leaves]
   const uint32_t* cat_words;      // categorical bitsets: [nwords, w0, w1, ...] per node
-  // compact layout (LDS-staged irregular trees)
-  const int64_t* cpt_off;         // [T+1] byte offset of each tree record in the image
-  const int32_t* cpt_nint;        // [T] internal nodes per tree
-  const int32_t* cpt_depth;       // [T] max depth per tree
-  const int32_t* cpt_root;        // [T] root child code (0, or kCptLeaf for a single leaf)
+  // staged record layouts (7, 9)
   const int32_t* stage_start;     // [n_stages+1] first tree of each LDS stage
   int32_t n_stages;
-  int32_t feat_shift;             // log2(R * sizeof(XT)): column stride of the LDS image
   // binned layouts: rank images of the features (see stage_bins)
   const void* bin_tbl;            // [F][2^bin_L] Eytzinger threshold tables, XT
   int32_t bin_L;                  // search depth (common to all features)
@@ -121,6 +112,7 @@ struct KArgs {
   int32_t bin_words;              // packed bin words per row (C)
   int32_t bin_chunk;              // columns binned per pass through the temp area
   int32_t stage_off;              // LDS byte offset of the tree stage / temp area
+  uint32_t bin_mask;              // binned heap: the node word's bin-offset bits
   // record explicit layout (6): 8-byte slots, first slot of each tree
   const uint2* rx_recs;           // [slots]
   const uint32_t* rx_base;        // [T] first slot of each tree
@@ -484,9 +476,17 @@ __global__ void __launch_bounds__(512) heap_predict_kernel(const KArgs a) {
 //     (f / P) * R * 4 + l * 4 + (f % P) * width,
 // so the lanes of a read hit 32 distinct banks whatever feature each tests.
 // A binned heap node is one u32: bits 0..14 that byte offset minus the lane
-// part, bit 15 NaN-left, bits 16..31 the rank.
+// part, bit 15 NaN-left, bits 16..31 the rank.  With 512-row tiles the offset
+// is word * 2048 + the byte of the word (bits 0, 1, 11..14) and the lane part
+// is tid * 4 (bits 2..10), so bits 3..10 are free in the image: they hold the
+// node's own heap index i (8 i = the byte offset of its children pair in the
+// record), which the fixed-layout walk (bheap_fix_kernel) uses as the pair
+// address.  a.bin_mask selects the offset bits (kBNodeOffMask512 then,
+// kBNodeOffMask for smaller tiles, whose images carry no index).
 constexpr uint32_t kBNodeNanLeft = 0x8000u;
 constexpr uint32_t kBNodeOffMask = 0x7FFFu;
+constexpr uint32_t kBNodeOffMask512 = 0x7803u;
+constexpr uint32_t kBNodePairMask = 0x7F8u;
 
 template <bool B16> struct BinTraits;
 template <> struct BinTraits<true> { static constexpr int P = 2; static constexpr uint32_t kNan = 0xFFFFu; };
@@ -508,25 +508,84 @@ __device__ __forceinline__ uint32_t lds_bin(uint32_t byte_addr) {
       static_cast<uintptr_t>(byte_addr));
 }
 
+__device__ __forceinline__ uint32_t kpow5(int h) {
+  uint32_t p = 1u;
+  for (int i = 0; i < h; ++i) p *= 5u;
+  return p;
+}
+
+// b[q] = 1 + #{u in U_f : u < x[q]} for Q consecutive features f0 + q (the
+// last feature repeated past F; NaN gives an unspecified b, the caller codes
+// it).  Two table forms (host: eytzinger_tables / kary_tables):
+//  * Eytzinger: 2^L entries per feature, node k's children 2k and 2k+1,
+//    +inf padded: L dependent 4- or 8-byte gathers;
+//  * 5-ary (float32 view, a.bin_kary = H > 0): node j holds 4 sorted keys in
+//    16 B, children 5j+1 .. 5j+5; after H levels j - (5^H - 1)/4 is the
+//    count: H dependent 16-byte gathers (C2: 6 instead of 13).
+// Q independent chains per lane hide the L2 latency of each level.
+template <typename XT, int Q>
+__device__ __forceinline__ void rank_search(const KArgs& a, const XT (&x)[Q], int f0,
+                                            uint32_t (&b)[Q]) {
+  const int F = a.n_features;
+  uint32_t tq[Q], k[Q];
+  if (sizeof(XT) == 4 && a.bin_kary > 0) {
+    typedef float f4_t __attribute__((ext_vector_type(4)));
+    const f4_t* t4 = reinterpret_cast<const f4_t*>(a.bin_tbl);
+    const uint32_t nn = (kpow5(a.bin_kary) - 1u) / 4u;   // nodes per feature
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      tq[q] = (uint32_t)(f0 + q < F ? f0 + q : F - 1) * nn;
+      k[q] = 0u;
+    }
+    for (int s = 0; s < a.bin_kary; ++s) {
+      f4_t e[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) e[q] = t4[tq[q] + k[q]];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const float xv = (float)x[q];
+        const uint32_t c = (e[q].x < xv ? 1u : 0u) + (e[q].y < xv ? 1u : 0u) +
+                           (e[q].z < xv ? 1u : 0u) + (e[q].w < xv ? 1u : 0u);
+        k[q] = 5u * k[q] + 1u + c;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) b[q] = 1u + k[q] - nn;
+  } else {
+    const XT* tbl = static_cast<const XT*>(a.bin_tbl);
+    const uint32_t tsz = 1u << a.bin_L;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      tq[q] = (uint32_t)(f0 + q < F ? f0 + q : F - 1) * tsz;   // element offset, not a pointer
+      k[q] = 1u;
+    }
+    for (int s = 0; s < a.bin_L; ++s) {
+      XT e[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) e[q] = tbl[tq[q] + k[q]];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) b[q] = 1u + k[q] - tsz;
+  }
+}
+
 // Bin the tile's rows into the LDS bin image (at LDS address 0).  Columns go
 // through `temp` (the tree-stage area, free at this point) bin_chunk at a
 // time: a coalesced copy into [c][R], then every lane searches its own row's
-// values in the Eytzinger tables (global, L2-resident: 2^L entries per
-// feature, node k's children 2k and 2k+1, padded with +inf), eight features
-// at once for eight independent load chains.  Returns (uniformly) whether a
-// live row of the tile holds a NaN.  Ends in a barrier.
-template <typename XT, bool B16>
+// values (rank_search), Q features at once for Q independent load chains.
+// Returns (uniformly) whether a live row of the tile holds a NaN.  Ends in a
+// barrier.
+template <typename XT, bool B16, int Q = TI_BIN_Q>
 __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const KArgs& a,
                                            int64_t row0, int R, int tid) {
   using BT = BinTraits<B16>;
   constexpr int P = BT::P;
-  constexpr int Q = TI_BIN_Q;   // features searched at once (a multiple of P)
+  static_assert(Q % P == 0, "features searched at once: a multiple of the bins per word");
   const XT* X = static_cast<const XT*>(a.X);
-  const XT* tbl = static_cast<const XT*>(a.bin_tbl);
   const int F = a.n_features;
   const int C = a.n_cols;
-  const int L = a.bin_L;
-  const uint32_t tsz = 1u << L;
   const int64_t left_rows = a.n_rows - row0;
   const int rows_here = left_rows < R ? (int)left_rows : R;
   const bool vec_ok = ((reinterpret_cast<uintptr_t>(X) | (uintptr_t)(a.row_stride * sizeof(XT))) & 15) == 0;
@@ -557,33 +616,16 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
       const uint32_t r = e / ukc;
       const uint32_t c = e - r * ukc;
       const int f = f0 + (int)c;
-#if TI_NT_X
-      const XT v = f < C ? __builtin_nontemporal_load(X + (row0 + r) * a.row_stride + f)
-                         : nan_value<XT>();
-#else
       const XT v = f < C ? X[(row0 + r) * a.row_stride + f] : nan_value<XT>();
-#endif
       temp[c * R + r] = zero_map(v, a.lgb_zero_map);
     }
     __syncthreads();
     for (int c = 0; c < kc; c += Q) {
       XT x[Q];
-      uint32_t tq[Q];   // the feature's table (element offset, not a pointer)
-      uint32_t k[Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int cc = c + q < kc ? c + q : kc - 1;
-        x[q] = temp[cc * R + tid];
-        tq[q] = (uint32_t)(f0 + cc) * tsz;
-        k[q] = 1u;
-      }
-      for (int s = 0; s < L; ++s) {
-        XT e[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) e[q] = tbl[tq[q] + k[q]];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
-      }
+      for (int q = 0; q < Q; ++q) x[q] = temp[(c + q < kc ? c + q : kc - 1) * R + tid];
+      uint32_t b[Q];
+      rank_search<XT, Q>(a, x, f0 + c, b);
       uint32_t w[Q / P];
 #pragma unroll
       for (int j = 0; j < Q / P; ++j) w[j] = 0u;
@@ -591,8 +633,7 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
       for (int q = 0; q < Q; ++q) {
         const bool nan = x[q] != x[q];
         has_nan |= nan && (c + q < kc);
-        const uint32_t b = nan ? BT::kNan : 1u + k[q] - tsz;
-        w[q / P] |= b << ((q % P) * (32 / P));
+        w[q / P] |= (nan ? BT::kNan : b[q]) << ((q % P) * (32 / P));
       }
 #pragma unroll
       for (int j = 0; j < Q / P; ++j) {
@@ -607,72 +648,6 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
     }
   }
   if (has_nan && tid < rows_here) *flag = 1;
-  __syncthreads();
-  return *flag != 0;
-}
-
-// Bin the tile without a temp area: every lane loads its own row's values
-// straight from global memory (neighbouring lanes share the row's cache
-// lines) and searches them as stage_bins does.  For kernels whose LDS holds
-// nothing else (the binned explicit kernel), so the bin image alone sets the
-// workgroups per CU.  Ends in a barrier; returns the tile's NaN flag.
-template <typename XT, bool B16>
-__device__ __forceinline__ bool stage_bins_rows(volatile int* flag, const KArgs& a, int64_t row0,
-                                                int R, int tid) {
-  using BT = BinTraits<B16>;
-  constexpr int P = BT::P;
-  constexpr int Q = 8;
-  const XT* tbl = static_cast<const XT*>(a.bin_tbl);
-  const int F = a.n_features;
-  const int FC = F < a.n_cols ? F : a.n_cols;
-  const int L = a.bin_L;
-  const uint32_t tsz = 1u << L;
-  const int64_t row = row0 + tid;
-  const bool live = row < a.n_rows;
-  const XT* xr = static_cast<const XT*>(a.X) + (live ? row : a.n_rows - 1) * a.row_stride;
-  bool has_nan = false;
-  if (tid == 0) *flag = 0;
-  for (int f0 = 0; f0 < F; f0 += Q) {
-    XT x[Q];
-    const XT* tq[Q];
-    uint32_t k[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int f = f0 + q < F ? f0 + q : F - 1;
-      x[q] = f0 + q < FC ? zero_map(xr[f], a.lgb_zero_map) : nan_value<XT>();
-      tq[q] = tbl + (size_t)f * tsz;
-      k[q] = 1u;
-    }
-    for (int s = 0; s < L; ++s) {
-      XT e[Q];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) e[q] = tq[q][k[q]];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
-    }
-    uint32_t w[Q / P];
-#pragma unroll
-    for (int j = 0; j < Q / P; ++j) w[j] = 0u;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const bool nan = x[q] != x[q];
-      has_nan |= nan && (f0 + q < F);
-      const uint32_t b = nan ? BT::kNan : 1u + k[q] - tsz;
-      w[q / P] |= b << ((q % P) * (32 / P));
-    }
-#pragma unroll
-    for (int j = 0; j < Q / P; ++j) {
-      const int word = f0 / P + j;
-      if (word < a.bin_words) {
-        __attribute__((address_space(3))) uint32_t* dst =
-            reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-                static_cast<uintptr_t>((uint32_t)(word * R + tid) * 4u));
-        *dst = w[j];
-      }
-    }
-  }
-  __syncthreads();   // flag = 0 is visible before any lane sets it
-  if (has_nan && live) *flag = 1;
   __syncthreads();
   return *flag != 0;
 }
@@ -709,7 +684,7 @@ __device__ __forceinline__ void bheap_stage(const KArgs& a, const unsigned char*
       uint2 pr[kBTilp];
 #pragma unroll
       for (int q = 0; q < kBTilp; ++q) {
-        b[q] = lds_bin<B16>((nd[q] & kBNodeOffMask) | lane_off);
+        b[q] = lds_bin<B16>((nd[q] & a.bin_mask) | lane_off);
         pr[q] = *reinterpret_cast<const uint2*>(tp[q] + 2u * idx[q]);
       }
 #pragma unroll
@@ -868,124 +843,140 @@ __global__ void __launch_bounds__(512) bheap_predict_kernel(const KArgs a) {
   finish_row<ACC, KMAX>(acc, a, row);
 }
 
-// ------------------------------------------------------------ compact kernel
-// Irregular trees with <= 512 internal nodes and <= 512 leaves (LightGBM
-// leaf-wise).  A tree record is {internal nodes[n_int], leaves[n_leaf * LW]};
-// a node is {thr, w}: w bits 0..9 feature, 10..19 left code, 20..29 right
-// code (code < 512: internal node, >= 512: leaf code-512), bit 30 zero flip,
-// bit 31 NaN-left.  Records are staged into LDS like the heap layout; each lane
-// walks kTilp trees for max-depth-of-group steps (a lane that reached a leaf
-// keeps its code), leaving early once every lane of the wave is at a leaf.
-template <typename XT, typename ACC, int KMAX, bool FEAT_LDS, bool ZERO, bool CHECK_NAN>
-__device__ __forceinline__ void compact_stage(const KArgs& a, const unsigned char* stage,
-                                              int64_t stage_base, int t0, int cnt,
-                                              ACC (&acc)[KMAX], uint32_t lane_off,
-                                              const unsigned char* xrow, int64_t row, bool live) {
-  using Node = HeapNode<XT>;
-  const int T = a.n_trees;
-  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
-  const uint32_t col_limit = (uint32_t)a.n_cols;
-  for (int j = 0; j < cnt; j += kTilp) {
-    const Node* tp[kTilp];
-    uint32_t code[kTilp];
-    int dmax = 0;
+// ---- binned heap, fixed layout (C2: depth 8, scalar float leaves) ---------
+// The same walk with compile-time LDS addresses.  A tile is 512 rows; the LDS
+// is [bin image (<= 14 words x 2 KB)][flag @ kFixFlag][stage @ kFixStage: NG
+// groups of 4 tree records of 2 KB].  Tree q of group g sits at the constant
+// kFixStage + (4 g + q) * 2048, so the children pair of the current node is
+// read at (nd & kBNodePairMask) + that constant (the node word carries its own
+// heap index in bits 3..10, pack_bheap): no index register and no address
+// arithmetic beyond one v_and_b32 with a literal.  A level is then
+//   v_and_or_b32 (bin address), v_and_b32 (pair address),
+//   ds_read_u16 / ds_read_u8 + ds_read_b64 (issued together),
+//   v_cmp_lt_u32_sdwa (rank < bin), v_cndmask_b32 (next node word)
+// = 4 VALU instead of 5, and the v_lshl_add / v_addc pair that the index
+// cost is gone (scripts/micro/valu_rate.hip: 6.6 vs 9.6 cycles per step per
+// SIMD at 8 waves).  At the last level the pair holds two leaves, so the
+// selected word is the leaf value.  Leaves are added in tree order, so the
+// float32 sums are xgboost's.  The host takes this kernel for float32
+// accumulators, one leaf value per leaf, depth-8 images of 512-row tiles and
+// <= 14 bin words; leaf ids (TI_OUTPUT_LEAF) keep bheap_predict_kernel.
+constexpr uint32_t kFixFlag = 28672u;
+constexpr uint32_t kFixStage = 30720u;
+constexpr int kFixRows = 512;
+constexpr int kFixTree = 2048;   // 256 node words + 256 float leaves
+
+__device__ __forceinline__ uint2 lds_u2c(uint32_t byte_addr) {
+  const uint64_t v = *reinterpret_cast<const __attribute__((address_space(3))) uint64_t*>(
+      static_cast<uintptr_t>(byte_addr));
+  return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+__device__ __forceinline__ uint32_t lds_u32(uint32_t byte_addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+      static_cast<uintptr_t>(byte_addr));
+}
+
+template <int KMAX, bool B16, bool CHECK_NAN, int NG>
+__device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0, float (&acc)[KMAX],
+                                                uint32_t lane_off) {
+  const uint32_t bmask = a.bin_mask;
 #pragma unroll
-    for (int q = 0; q < kTilp; ++q) {
-      const int tq = t0 + ((j + q) < cnt ? (j + q) : (cnt - 1));
-      tp[q] = reinterpret_cast<const Node*>(stage + (a.cpt_off[tq] - stage_base));
-      code[q] = (uint32_t)a.cpt_root[tq];
-      const int d = a.cpt_depth[tq];
-      dmax = d > dmax ? d : dmax;
-    }
-    for (int l = 0; l < dmax; ++l) {
-      XT thr[kTilp];
-      uint32_t w[kTilp];
+  for (int g = 0; g < NG; ++g) {
+    if (g * 4 >= cnt) break;   // uniform: the last stage may be short
+    uint32_t nd[4];
 #pragma unroll
-      for (int q = 0; q < kTilp; ++q) load_node(tp[q] + (code[q] & (kCptLeaf - 1u)), thr[q], w[q]);
-      XT x[kTilp];
+    for (int q = 0; q < 4; ++q) nd[q] = lds_u32(kFixStage + (uint32_t)((g * 4 + q) * kFixTree) + 4u);
 #pragma unroll
-      for (int q = 0; q < kTilp; ++q) {
-        const uint32_t f = w[q] & 0x3FFu;
-        if (FEAT_LDS) {
-          x[q] = lds_at<XT>((f << a.feat_shift) | lane_off);
+    for (int l = 0; l < 8; ++l) {
+      uint32_t b[4];
+      uint2 pr[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        b[q] = lds_bin<B16>((nd[q] & bmask) | lane_off);
+        pr[q] = lds_u2c((nd[q] & kBNodePairMask) + (kFixStage + (uint32_t)((g * 4 + q) * kFixTree)));
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!CHECK_NAN) {
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+              "v_cndmask_b32 %0, %2, %3, vcc"
+              : "+v"(nd[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y) : "vcc");
         } else {
-          x[q] = f < col_limit ? zero_map(reinterpret_cast<const XT*>(xrow)[f], a.lgb_zero_map)
-                               : nan_value<XT>();
+          // right = (rank < bin) && !(bin == NaN code && NaN-left (bit 15))
+          uint64_t mn, ml;
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %3 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+              "v_cmp_eq_u32_e64 %1, %6, %3\n\t"
+              "v_cmp_gt_i16_e64 %2, 0, %0\n\t"
+              "s_and_b64 %1, %1, %2\n\t"
+              "s_andn2_b64 vcc, vcc, %1\n\t"
+              "v_cndmask_b32 %0, %4, %5, vcc"
+              : "+v"(nd[q]), "=&s"(mn), "=&s"(ml)
+              : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y), "s"(BinTraits<B16>::kNan)
+              : "vcc", "scc");
         }
       }
-      bool active = false;
-#pragma unroll
-      for (int q = 0; q < kTilp; ++q) {
-        const bool left = go_left<ZERO, CHECK_NAN>(x[q], thr[q], w[q]);
-        const uint32_t child = (w[q] >> (left ? 10u : 20u)) & 0x3FFu;
-        code[q] = code[q] >= kCptLeaf ? code[q] : child;
-        active |= code[q] < kCptLeaf;
-      }
-      if (__ballot(active) == 0) break;   // wave-uniform early exit
     }
 #pragma unroll
-    for (int q = 0; q < kTilp; ++q) {
-      if (j + q < cnt) {
-        const int t = t0 + j + q;
-        const int leaf = (int)(code[q] - kCptLeaf);
-        if (want_leaf) {
-          if (live) static_cast<int32_t*>(a.out)[row * T + t] = a.exp_leaf_ids[a.leaf_base[t] + leaf];
-        } else {
-          const ACC* lv = reinterpret_cast<const ACC*>(tp[q] + a.cpt_nint[t]);
-          add_leaf<ACC, KMAX>(acc, lv, leaf, a.leaf_width, a.tree_group[t]);
-        }
+    for (int q = 0; q < 4; ++q) {
+      const int t = t0 + g * 4 + q;
+      if (g * 4 + q < cnt) {
+        const float v = __uint_as_float(nd[q]);   // the leaf the last level selected
+        add_leaf<float, KMAX>(acc, &v, 0, 1, KMAX == 1 ? 0 : a.tree_group[t]);
       }
     }
   }
 }
 
-template <typename XT, typename ACC, int KMAX, bool FEAT_LDS, bool ZERO>
-__global__ void __launch_bounds__(512) compact_predict_kernel(const KArgs a) {
+template <typename XT, int KMAX, bool B16, int NG>
+__global__ void __launch_bounds__(512) bheap_fix_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int R = blockDim.x;
+  constexpr int R = kFixRows;
+  constexpr int S = 4 * NG;   // trees per stage
   const int tid = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * R;
   const int64_t row = row0 + tid;
   const bool live = row < a.n_rows;
-  const size_t feat_bytes = FEAT_LDS ? align16((size_t)a.n_features * R * sizeof(XT)) : 0;
-  volatile int* flag = reinterpret_cast<volatile int*>(smem + feat_bytes);
-  unsigned char* stage = smem + feat_bytes + 16;
-  const unsigned char* xrow = reinterpret_cast<const unsigned char*>(
-      static_cast<const XT*>(a.X) + (live ? row : a.n_rows - 1) * a.row_stride);
-  const uint32_t lane_off = (uint32_t)tid * (uint32_t)sizeof(XT);
-  const bool tile_nan =
-      FEAT_LDS ? stage_features<XT>(reinterpret_cast<XT*>(smem), flag, a, row0, R, tid) : true;
-
-  ACC acc[KMAX];
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + kFixFlag);
+  u32x4* stage = reinterpret_cast<u32x4*>(smem + kFixStage);
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  const int T = a.n_trees;
+  constexpr int n16 = S * kFixTree / 16;   // 16-byte words per stage: NG per thread
+  static_assert(n16 == NG * R, "one 16-byte word per thread and group");
+  const u32x4* src = reinterpret_cast<const u32x4*>(a.trees);
+  const int n16_all = (int)(((int64_t)T * kFixTree) >> 4);
+  // first stage in flight while the tile is binned (a clamped lane re-reads
+  // the forest's last word; its stage slot then holds a word no tree reads)
+  u32x4 pf[NG];
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    const int i = tid + u * R;
+    pf[u] = src[i < n16_all ? i : n16_all - 1];
+  }
+  const bool tile_nan = stage_bins<XT, B16, 4 * NG>(
+      flag, reinterpret_cast<XT*>(smem + kFixStage), a, row0, R, tid);
+  float acc[KMAX];
   init_acc(acc, a);
-
-  const int NS = a.n_stages;
-  auto words = [&](int s) {
-    return (int)((a.cpt_off[a.stage_start[s + 1]] - a.cpt_off[a.stage_start[s]]) >> 4);
-  };
-  u32x4 pf[kPf];
-  prefetch_stage(pf, reinterpret_cast<const u32x4*>(a.trees), words(0), tid, R);
-  for (int s = 0; s < NS; ++s) {
-    const int t0 = a.stage_start[s];
-    const int cnt = a.stage_start[s + 1] - t0;
-    const int64_t base = a.cpt_off[t0];
+  for (int t0 = 0; t0 < T; t0 += S) {
+    const int cnt = (T - t0) < S ? (T - t0) : S;
     __syncthreads();
-    commit_stage(pf, reinterpret_cast<u32x4*>(stage), words(s), tid, R);
+#pragma unroll
+    for (int u = 0; u < NG; ++u) stage[tid + u * R] = pf[u];
     __syncthreads();
     {
-      const int sn = s + 1 < NS ? s + 1 : s;
-      prefetch_stage(pf, reinterpret_cast<const u32x4*>(a.trees + a.cpt_off[a.stage_start[sn]]),
-                     words(sn), tid, R);
+      const int base = (t0 + S) * (kFixTree / 16);
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        const int i = base + tid + u * R;
+        pf[u] = src[i < n16_all ? i : n16_all - 1];
+      }
     }
     if (tile_nan)
-      compact_stage<XT, ACC, KMAX, FEAT_LDS, ZERO, true>(a, stage, base, t0, cnt, acc, lane_off,
-                                                         xrow, row, live);
+      bheap_fix_stage<KMAX, B16, true, NG>(a, cnt, t0, acc, lane_off);
     else
-      compact_stage<XT, ACC, KMAX, FEAT_LDS, ZERO, false>(a, stage, base, t0, cnt, acc, lane_off,
-                                                          xrow, row, live);
+      bheap_fix_stage<KMAX, B16, false, NG>(a, cnt, t0, acc, lane_off);
   }
-  if (!live || a.kind == TI_OUTPUT_LEAF) return;
-  finish_row<ACC, KMAX>(acc, a, row);
+  if (!live) return;
+  finish_row<float, KMAX>(acc, a, row);
 }
 
 // ------------------------------------------------------------ explicit kernel
@@ -1072,205 +1063,6 @@ __global__ void __launch_bounds__(512) explicit_predict_kernel(const KArgs a) {
   finish_row<ACC, KMAX>(acc, a, row);
 }
 
-// ----------------------------------------------------- binned explicit kernel
-// The explicit kernel on a rank-binned feature image (any tree shape, nodes
-// in global memory).  A node is {rank | zbin << 16, offset | NaN-left (31) |
-// zero-flip (30), left, right}; offset is the feature's byte offset in the
-// bin image (without the lane part).  Split rule on bins (treeinfer.hip,
-// collect_ranks): left iff b <= rank, flipped when b == zbin (exact 0 on a
-// LightGBM zero-missing node; zbin = 0 on other nodes, and bins are >= 1),
-// and NaN (the top code) takes the NaN-left bit.  ILP trees are walked in
-// lockstep per lane: more of them hide more L2 latency but wait longer for the
-// deepest path of the group (the host picks 8 for shallow-on-average forests,
-// 4 for deep balanced ones).
-template <typename XT, typename ACC, int KMAX, bool B16, bool ZERO, int ILP>
-__global__ void __launch_bounds__(512) bexplicit_predict_kernel(const KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using BT = BinTraits<B16>;
-  const int R = blockDim.x;
-  const int tid = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * R;
-  const int64_t row = row0 + tid;
-  const bool live = row < a.n_rows;
-  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
-  const bool tile_nan = stage_bins_rows<XT, B16>(flag, a, row0, R, tid);
-  const uint32_t lane_off = (uint32_t)tid * 4u;
-  const int T = a.n_trees;
-  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
-  int32_t* out_leaf = static_cast<int32_t*>(a.out);
-  const ACC* leaves = static_cast<const ACC*>(a.leaves);
-
-  ACC acc[KMAX];
-  init_acc(acc, a);
-
-  for (int t0 = 0; t0 < T; t0 += ILP) {
-    int64_t nb[ILP];
-    int32_t c[ILP];
-#pragma unroll
-    for (int q = 0; q < ILP; ++q) {
-      const int tq = (t0 + q) < T ? (t0 + q) : (T - 1);
-      nb[q] = a.node_base[tq];
-      c[q] = a.root[tq];
-    }
-    for (;;) {
-      u32x4 nd[ILP];
-#pragma unroll
-      for (int q = 0; q < ILP; ++q)
-        nd[q] = *reinterpret_cast<const u32x4*>(a.nodes + nb[q] + (c[q] < 0 ? 0 : c[q]));
-      uint32_t b[ILP];
-#pragma unroll
-      for (int q = 0; q < ILP; ++q) b[q] = lds_bin<B16>((nd[q].y & kMetaFeatMask) | lane_off);
-      bool active = false;
-#pragma unroll
-      for (int q = 0; q < ILP; ++q) {
-        bool l = b[q] <= (nd[q].x & 0xFFFFu);
-        if (ZERO) l = l != (b[q] == (nd[q].x >> 16));
-        if (tile_nan && b[q] == BT::kNan) l = (int32_t)nd[q].y < 0;
-        const int32_t next = l ? (int32_t)nd[q].z : (int32_t)nd[q].w;
-        c[q] = c[q] < 0 ? c[q] : next;
-        active |= c[q] >= 0;
-      }
-      if (__ballot(active) == 0) break;
-    }
-#pragma unroll
-    for (int q = 0; q < ILP; ++q) {
-      const int t = t0 + q;
-      if (t < T) {
-        const int64_t lb = a.leaf_base[t];
-        if (want_leaf) {
-          if (live) out_leaf[row * T + t] = a.exp_leaf_ids[lb + (~c[q])];
-        } else {
-          add_leaf<ACC, KMAX>(acc, leaves + lb * a.leaf_width, ~c[q], a.leaf_width,
-                              a.tree_group[t]);
-        }
-      }
-    }
-  }
-  if (!live || want_leaf) return;
-  finish_row<ACC, KMAX>(acc, a, row);
-}
-
-// ---- staged binned explicit (layout 5) -------------------------------------
-// Irregular trees small enough to stage in LDS (LightGBM leaf-wise, C3): the
-// binned explicit walk of bexplicit_predict_kernel with the nodes read from an
-// LDS stage instead of global memory, so a step is two LDS reads and ~6 VALU
-// instead of a 16-byte gather through the vector L1 (the gathers bounded the
-// global-memory walk: 54 % of wave cycles waiting, rocprofv3 C3 profile).
-//
-// A tree record is tree_stride / 8 slots of 8 bytes.  Slot 0 is the root and
-// the two children of an internal node sit in consecutive slots (left, then
-// right), so the next slot is left + (went right).  Internal slot:
-//   x = rank << 16 | bin byte offset (the lane-free part, as in bheap);
-//   y = zbin << 16 | NaN-left << 15 | left child slot (15 bits).
-// Leaf slot: x = kSxLeaf (rank 0xFFFF: no bin goes right of it), y = NaN-left
-// | its own slot, so a lane that reached its leaf stays on it while the rest of
-// the wave finishes the tree group.  Leaf values / ids are per-slot global
-// tables ([T][slots]), read once per tree.
-constexpr uint32_t kSxLeaf = 0xFFFF0000u;
-constexpr uint32_t kSxNanLeft = 0x8000u;
-constexpr uint32_t kSxSlotMask = 0x7FFFu;
-
-struct SxRec {
-  uint32_t x, y;
-};
-__device__ __forceinline__ SxRec lds_u2(uint32_t byte_addr) {
-  const uint64_t v = *reinterpret_cast<const __attribute__((address_space(3))) uint64_t*>(
-      static_cast<uintptr_t>(byte_addr));
-  return SxRec{(uint32_t)v, (uint32_t)(v >> 32)};
-}
-
-template <typename ACC, int KMAX, bool B16, bool ZERO, bool CHECK_NAN, int ILP>
-__device__ __forceinline__ void sx_stage(const KArgs& a, int cnt, int t0, ACC (&acc)[KMAX],
-                                         uint32_t lane_off, int64_t row, bool live) {
-  using BT = BinTraits<B16>;
-  const int T = a.n_trees;
-  const uint32_t stride = (uint32_t)a.tree_stride;
-  const int64_t nslot = a.tree_stride >> 3;
-  const bool want_leaf = a.kind == TI_OUTPUT_LEAF;
-  const ACC* vals = static_cast<const ACC*>(a.leaves);
-  for (int j = 0; j < cnt; j += ILP) {
-    uint32_t base[ILP], slot[ILP];
-    SxRec rec[ILP];
-#pragma unroll
-    for (int q = 0; q < ILP; ++q) {
-      const int tq = (j + q) < cnt ? (j + q) : (cnt - 1);
-      base[q] = (uint32_t)a.stage_off + (uint32_t)tq * stride;
-      slot[q] = 0u;
-      rec[q] = lds_u2(base[q]);
-    }
-    for (;;) {
-      uint32_t b[ILP];
-#pragma unroll
-      for (int q = 0; q < ILP; ++q) b[q] = lds_bin<B16>((rec[q].x & 0xFFFFu) | lane_off);
-      bool active = false;
-#pragma unroll
-      for (int q = 0; q < ILP; ++q) {
-        bool right = (rec[q].x >> 16) < b[q];
-        if (ZERO) right = right != (b[q] == (rec[q].y >> 16));
-        if (CHECK_NAN && b[q] == BT::kNan) right = (rec[q].y & kSxNanLeft) == 0u;
-        slot[q] = (rec[q].y & kSxSlotMask) + (right ? 1u : 0u);
-        rec[q] = lds_u2(base[q] + slot[q] * 8u);
-        active |= rec[q].x < kSxLeaf;
-      }
-      if (__ballot(active) == 0) break;
-    }
-#pragma unroll
-    for (int q = 0; q < ILP; ++q) {
-      if (j + q < cnt) {
-        const int t = t0 + j + q;
-        if (want_leaf) {
-          if (live) static_cast<int32_t*>(a.out)[row * T + t] = a.exp_leaf_ids[(int64_t)t * nslot + slot[q]];
-        } else {
-          add_leaf<ACC, KMAX>(acc, vals + (int64_t)t * nslot * a.leaf_width, (int)slot[q],
-                              a.leaf_width, a.tree_group[t]);
-        }
-      }
-    }
-  }
-}
-
-template <typename XT, typename ACC, int KMAX, bool B16, bool ZERO, int ILP>
-__global__ void __launch_bounds__(256) sexplicit_predict_kernel(const KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int PF = 8;
-  const int R = blockDim.x;
-  const int tid = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * R;
-  const int64_t row = row0 + tid;
-  const bool live = row < a.n_rows;
-  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
-  unsigned char* stage = smem + a.stage_off;
-  const uint32_t lane_off = (uint32_t)tid * 4u;
-  const int T = a.n_trees;
-  const int S = a.stage_trees;
-  const int64_t stride = a.tree_stride;
-  u32x4 pf[PF];
-  prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees),
-                 (int)(((int64_t)(T < S ? T : S) * stride) >> 4), tid, R);
-  const bool tile_nan = stage_bins_rows<XT, B16>(flag, a, row0, R, tid);
-  ACC acc[KMAX];
-  init_acc(acc, a);
-  const int last0 = ((T - 1) / S) * S;
-  for (int t0 = 0; t0 < T; t0 += S) {
-    const int cnt = (T - t0) < S ? (T - t0) : S;
-    __syncthreads();
-    commit_n<PF>(pf, reinterpret_cast<u32x4*>(stage), (int)(((int64_t)cnt * stride) >> 4), tid, R);
-    __syncthreads();
-    {
-      const int tn = t0 + S <= last0 ? t0 + S : last0;
-      const int cn = (T - tn) < S ? (T - tn) : S;
-      prefetch_n<PF>(pf, reinterpret_cast<const u32x4*>(a.trees + (int64_t)tn * stride),
-                     (int)(((int64_t)cn * stride) >> 4), tid, R);
-    }
-    if (tile_nan)
-      sx_stage<ACC, KMAX, B16, ZERO, true, ILP>(a, cnt, t0, acc, lane_off, row, live);
-    else
-      sx_stage<ACC, KMAX, B16, ZERO, false, ILP>(a, cnt, t0, acc, lane_off, row, live);
-  }
-  if (!live || a.kind == TI_OUTPUT_LEAF) return;
-  finish_row<ACC, KMAX>(acc, a, row);
-}
-
 // ---- record explicit (layout 6) --------------------------------------------
 // Deep / irregular trees (LightGBM leaf-wise C3, sklearn depth 16 C4).  What
 // bounds a walk whose nodes come from L2 is the vector-memory pipe, not the
@@ -1354,7 +1146,7 @@ __device__ __forceinline__ uint16_t lds_u16(uint32_t byte_addr) {
       static_cast<uintptr_t>(byte_addr));
 }
 
-// Bin the tile's rows (as stage_bins_rows, one lane per row, per-lane loads)
+// Bin the tile's rows (one lane per row, per-lane loads)
 // into the u16 image of layouts 6 / 7: b = 1 + #{u < x}, NaN = 0xFFFF; with ZB
 // (zero-missing forests) b2 = 2 b + (x == 0) and NaN = 0xFFFE.  Returns
 // (uniformly) whether the tile needs the slow step: a NaN, or with ZB an
@@ -1367,12 +1159,6 @@ __device__ __forceinline__ uint16_t lds_u16(uint32_t byte_addr) {
 #define TI_RX_BINQ 8   // features searched at once per lane (independent load chains;
                        // 16 measured slower on C3 and C4)
 #endif
-__device__ __forceinline__ uint32_t kpow5(int h) {
-  uint32_t p = 1u;
-  for (int i = 0; i < h; ++i) p *= 5u;
-  return p;
-}
-
 // Search Q consecutive features [f0, f0 + Q) of the lane's row (values x,
 // NaN past the last feature) and store their packed u16 bins in the image
 // (f0 even).  With ZB (zero-missing forests) b2 = 2 b + (x == 0), NaN 0xFFFE.

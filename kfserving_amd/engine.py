@@ -83,6 +83,8 @@ class _ForestInfo(ctypes.Structure):
         ("n_devices", ctypes.c_int32),
         ("device_bytes", ctypes.c_int64),
         ("tree_stride_bytes", ctypes.c_int64),
+        ("walk", ctypes.c_int32),
+        ("bin_bits", ctypes.c_int32),
     ]
 
 

@@ -276,7 +276,9 @@ class Application:
         except v2.V2Error as e:
             return bad(str(e))
         if self._batcher_factory is not None:
-            key = (name, "tensor")
+            # one batcher per column count: a request of another width never
+            # lands in (and fails) a batch of well-formed ones; it fails alone
+            key = (name, "tensor", X.shape[1])
             batcher = self._batchers.get(key)
             if batcher is None or batcher.model is not model:
                 batcher = self._batcher_factory(model, self._call, "tensor")

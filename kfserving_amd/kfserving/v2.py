@@ -75,8 +75,14 @@ def split_body(headers: Mapping[str, str], body: bytes) -> Tuple[bytes, bytes]:
 
 def _shape(t: Dict) -> Tuple[int, ...]:
     shape = t.get("shape")
-    if not isinstance(shape, list) or not all(isinstance(d, int) and d >= 0 for d in shape):
+    if not isinstance(shape, list) or not all(
+            isinstance(d, int) and not isinstance(d, bool) and d >= 0 for d in shape):
         raise V2Error(f"input {t.get('name')!r}: shape must be a list of non-negative integers")
+    count = 1
+    for d in shape:           # Python ints: a product past int64 is an error, not a wrap
+        count *= d
+    if count >= 1 << 62:
+        raise V2Error(f"input {t.get('name')!r}: shape {shape} is too large")
     return tuple(shape)
 
 
@@ -90,27 +96,36 @@ def decode_inputs(req: Dict, tail: bytes) -> List[Tuple[str, np.ndarray]]:
         if dt is None:
             raise V2Error(f"input {name!r}: unsupported datatype {t.get('datatype')!r}")
         shape = _shape(t)
-        count = int(np.prod(shape, dtype=np.int64)) if shape else 1
+        count = 1
+        for d in shape:
+            count *= d
         params = t.get("parameters") or {}
         size = params.get("binary_data_size") if isinstance(params, dict) else None
         if size is not None:
             want = count * np.dtype(dt).itemsize
-            if size != want or off + size > len(tail):
-                raise V2Error(f"input {name!r}: binary_data_size {size} does not match "
+            if (not isinstance(size, int) or isinstance(size, bool) or size != want
+                    or off + size > len(tail)):
+                raise V2Error(f"input {name!r}: binary_data_size {size!r} does not match "
                               f"shape {list(shape)} x {t['datatype']} ({want} bytes) or the body")
-            arr = np.frombuffer(tail, dtype=np.dtype(dt).newbyteorder("<"), count=count,
-                                offset=off).reshape(shape)
+            try:
+                arr = np.frombuffer(tail, dtype=np.dtype(dt).newbyteorder("<"), count=count,
+                                    offset=off).reshape(shape)
+            except (TypeError, ValueError, OverflowError) as e:
+                raise V2Error(f"input {name!r}: cannot read {list(shape)} x {t['datatype']}: {e}")
             off += size
         else:
             if "data" not in t:
                 raise V2Error(f"input {name!r}: no data")
             try:
                 arr = np.asarray(t["data"], dtype=dt)
-            except (TypeError, ValueError) as e:
+            except (TypeError, ValueError, OverflowError) as e:
                 raise V2Error(f"input {name!r}: data is not {t['datatype']}: {e}")
             if arr.size != count:
                 raise V2Error(f"input {name!r}: {arr.size} values for shape {list(shape)}")
-            arr = arr.reshape(shape)
+            try:
+                arr = arr.reshape(shape)
+            except (TypeError, ValueError, OverflowError) as e:
+                raise V2Error(f"input {name!r}: cannot reshape to {list(shape)}: {e}")
         out.append((name, arr))
     if off != len(tail):
         raise V2Error(f"{len(tail) - off} bytes of binary data belong to no input")

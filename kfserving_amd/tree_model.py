@@ -106,14 +106,23 @@ def xgb_matrix_from_list(instances) -> np.ndarray:
 
 
 def _numeric_column(values) -> bool:
-    seen_number = False
+    """Whether pandas types the column as a number or bool dtype: all bool
+    (no None), or int / float with None allowed beside at least one number.
+    Mixed bool / number and bool + None columns are object dtype, which
+    lightgbm's dtype check rejects: those take the pandas path."""
+    n_bool = n_num = n_none = 0
     for v in values:
         if v is None:
-            continue
-        if not isinstance(v, (bool, int, float)):
+            n_none += 1
+        elif isinstance(v, bool):
+            n_bool += 1
+        elif isinstance(v, (int, float)):
+            n_num += 1
+        else:
             return False
-        seen_number = True
-    return seen_number or len(values) == 0
+    if n_bool:
+        return n_num == 0 and n_none == 0
+    return n_num > 0 or len(values) == 0
 
 
 def lgb_matrix_from_inputs(inputs: List[dict], feature_names: List[str]) -> np.ndarray:

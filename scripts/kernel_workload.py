@@ -1,0 +1,76 @@
+"""One named workload's predict kernel on one GPU, for rocprofv3 passes
+(scripts/kernel_pmc.sh) and quick timings: the forest and device-resident
+N(0,1) batch of bench.py's config, --steps launches of OUT_PREDICT on the
+launch stream, one JSON line with the event time per launch.
+
+  c2         500 x depth-8 XGBoost binary, 28 features, float32 (bench headline)
+  c3 / c3_f64  LightGBM leaf-wise 1000 x 255 leaves, 100 features, float32 /
+             float64 input (lgbserver's DataFrame dtype)
+  c3_maxbin  the LightGBM-shaped variant (thresholds on 255 quantile bin edges,
+             nested along each path; lightgbm_format.synthetic_maxbin_trees)
+  c4         the cached sklearn RandomForestRegressor 200 x depth 16, 64 features
+
+Usage: python scripts/kernel_workload.py --workload c3 [--rows 1000000] [--steps 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def forest_of(workload):
+    import bench
+    if workload == "c2":
+        return bench.build_model()[2], bench.N_FEAT, "float32"
+    if workload in ("c3", "c3_f64"):
+        return bench.c3_forest()[0], 100, "float64" if workload == "c3_f64" else "float32"
+    if workload == "c3_maxbin":
+        return bench.c3_maxbin_forest()[0], 100, "float32"
+    if workload == "c4":
+        return bench.c4_forest()[0], 64, "float32"
+    raise ValueError(workload)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--workload", required=True)
+    p.add_argument("--rows", type=int, default=1_000_000)
+    p.add_argument("--steps", type=int, default=3)
+    a = p.parse_args()
+    import torch
+    import bench
+    from kfserving_amd.engine import DeviceForest
+    from kfserving_amd.forest import OUT_PREDICT, TI_F32, TI_F64
+    forest, F, dtype = forest_of(a.workload)
+    dev = DeviceForest(forest, [0])
+    X = bench.device_normal(a.rows, F, 3, "cuda:0", dtype)
+    xdt = TI_F64 if dtype == "float64" else TI_F32
+    out = torch.empty(a.rows * forest.output_width(OUT_PREDICT),
+                      dtype=torch.float64 if forest.accum_dtype else torch.float32, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        dev.predict_device(X.data_ptr(), xdt, a.rows, F, F, OUT_PREDICT, out.data_ptr(),
+                           out.numel(), stream=sh)
+    step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.steps):
+        step()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.steps
+    info = dev.info()
+    print(json.dumps({"workload": a.workload, "rows": a.rows, "dtype": dtype,
+                      "layout": bench.LAYOUT_NAMES.get(info["layout"]), "walk": info["walk"],
+                      "bin_bits": info["bin_bits"], "kernel_ms": ms,
+                      "rows_per_s": a.rows / (ms * 1e-3)}), flush=True)
+    dev.close()
+
+
+if __name__ == "__main__":
+    main()

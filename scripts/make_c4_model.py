@@ -44,6 +44,69 @@ def fit(rows: int, jobs: int, n_estimators: int = 200):
                                  random_state=0, n_jobs=jobs).fit(X, y)
 
 
+def sklearn_estimator(path: str = MODEL):
+    """sklearn's own RandomForestRegressor rebuilt from the cached tree arrays
+    (no pickle, no refit): each member's ``tree_`` is restored through
+    ``Tree.__setstate__`` from the arrays the fit produced, so ``predict`` is
+    the library's own code on the fitted model (bench.py's C4 CPU baseline).
+    The node fields predict never reads (impurity, sample counts) are zero;
+    ``weighted_n_node_samples`` is the cached cover.  check() proves the
+    rebuilt estimator answers exactly what the fitted one did."""
+    from sklearn.ensemble import RandomForestRegressor
+    from sklearn.tree import DecisionTreeRegressor
+    from sklearn.tree._tree import Tree
+    z = np.load(path, allow_pickle=False)
+    T, F = int(z["n_trees"]), int(z["n_features"])
+    est = RandomForestRegressor(n_estimators=T, max_depth=16, max_features=1 / 3, random_state=0)
+    members = []
+    for i in range(T):
+        left = z[f"t{i}_children_left"]
+        n = left.shape[0]
+        nodes = np.zeros(n, dtype=[("left_child", "<i8"), ("right_child", "<i8"),
+                                   ("feature", "<i8"), ("threshold", "<f8"),
+                                   ("impurity", "<f8"), ("n_node_samples", "<i8"),
+                                   ("weighted_n_node_samples", "<f8"),
+                                   ("missing_go_to_left", "u1")])
+        nodes["left_child"] = left
+        nodes["right_child"] = z[f"t{i}_children_right"]
+        nodes["feature"] = z[f"t{i}_feature"]
+        nodes["threshold"] = z[f"t{i}_threshold"]
+        nodes["missing_go_to_left"] = z[f"t{i}_missing_go_to_left"]
+        if f"t{i}_cover" in z.files:
+            nodes["weighted_n_node_samples"] = z[f"t{i}_cover"]
+        value = np.ascontiguousarray(z[f"t{i}_value"], dtype=np.float64)
+        depth = _depth(left, nodes["right_child"])
+        tree = Tree(F, np.array([1], dtype=np.intp), 1)
+        tree.__setstate__({"max_depth": depth, "node_count": n, "nodes": nodes, "values": value})
+        m = DecisionTreeRegressor(max_depth=16, max_features=1 / 3)
+        m.tree_ = tree
+        m.n_features_in_ = F
+        m.n_outputs_ = 1
+        m.max_features_ = max(1, int(F / 3))
+        members.append(m)
+    est.estimators_ = members
+    est.estimator_ = DecisionTreeRegressor()
+    est.n_features_in_ = F
+    est.n_outputs_ = 1
+    return est
+
+
+def _depth(left, right) -> int:
+    depth = np.zeros(left.shape[0], dtype=np.int64)
+    for j in range(left.shape[0]):     # children follow their parent in sklearn's order
+        if left[j] >= 0:
+            depth[left[j]] = depth[right[j]] = depth[j] + 1
+    return int(depth.max())
+
+
+def check(est) -> bool:
+    """The rebuilt estimator's predict on the cached check rows equals the
+    fitted estimator's, bit for bit (single thread: estimator order)."""
+    z = np.load(CHECK, allow_pickle=False)
+    est.set_params(n_jobs=1)
+    return bool(np.array_equal(est.predict(z["X"]), z["predict"]))
+
+
 def check_rows(n: int = 4096, seed: int = 2):
     rng = np.random.default_rng(seed)
     X = rng.standard_normal((n, 64)).astype(np.float32)

@@ -136,6 +136,9 @@ def test_threaded_rejects_what_one_thread_rejects():
         cases.append(body[:k] + "[" + body[k:])           # stray '[' (a nested row)
         cases.append(body[:e] + ",]" + body[e + 1:])      # trailing comma in a row
     cases.append(body + "x")
+    last_close = body.rstrip().rstrip("}").rstrip().rfind("]")    # the instances list's ']'
+    cases.append(body[:last_close] + "," + body[last_close:])     # trailing comma after the last row
+    cases.append(body[:last_close] + ", " + body[last_close:])
     cases.append(body.replace('"instances"', '"instance"', 1))
     cases.append(body.rstrip()[:-1])                       # no closing brace
     for bad in cases:

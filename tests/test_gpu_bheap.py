@@ -149,3 +149,67 @@ def test_bheap_lightgbm_float64_accumulation(dtype):
     X = X.astype(dtype)
     want = port.lgb_predict_raw(trees, 1, 20, X.astype(np.float64))[:, 0]
     assert np.array_equal(dev.predict(X, OUT_MARGIN), want)
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("ng", ["1", "2"])
+@pytest.mark.parametrize("quantize", [16, None], ids=["u8", "u16"])
+def test_bheap_fixed_walk(quantize, ng):
+    """The fixed-layout walk (bheap_fix_kernel: compile-time LDS addresses, the
+    pair address from the node word's heap index) against the oracle and the
+    indexed walk: a partial last stage (37 trees), shallow trees padded to
+    depth 8, NaN and NaN-free tiles, ragged tiles of the 512-row layout, one
+    and four stage groups, u8 and u16 bins, and a multiclass forest (tree
+    groups, KMAX 4)."""
+    deep, ti_d = xf.synthetic_complete_trees(30, 8, 28, seed=41)
+    shallow, ti_s = xf.synthetic_complete_trees(7, 3, 28, seed=42)
+    trees = deep[:20] + shallow + deep[20:]
+    ti = np.concatenate([ti_d[:20], ti_s, ti_d[20:]])
+    if quantize:                                    # <= 253 thresholds per feature: u8 bins
+        for t in trees:
+            v = t["value"][:int((t["cleft"] >= 0).sum())]
+            v[:] = np.round(v * quantize) / quantize
+    forest = xf.forest_from_raw_trees(trees, ti, 28, 0, 0.5, "binary:logistic")
+    ref = xgb_ref.from_raw_trees(trees, ti, 28, 0, 0.5, "binary:logistic")
+    env = {"TI_BHEAP_NG": ng}
+    dev = _with_env(env, lambda: DeviceForest(forest, [0]))
+    inf = dev.info()
+    assert inf["layout"] == BHEAP and inf["walk"] == 1 and inf["depth"] == 8
+    assert inf["bin_bits"] == (8 if quantize else 16)
+    for rows in (1, 511, 512, 513, 4097):
+        X = _edge_rows(deep, 8, 28, rows, seed=rows + 3)
+        got = _with_env(env, lambda: dev.predict(X, OUT_MARGIN))
+        assert np.array_equal(got, xgb_ref.predict(ref, X, output_margin=True)), rows
+        np.testing.assert_allclose(_with_env(env, lambda: dev.predict(X, OUT_PREDICT)),
+                                   xgb_ref.predict(ref, X), rtol=1e-5, atol=0)
+        idx = _with_env({"TI_BHEAP_FIX": "0"}, lambda: dev.predict(X, OUT_MARGIN))
+        assert np.array_equal(got, idx)
+    X = _edge_rows(deep, 8, 28, 3000, seed=9)
+    X[~np.isfinite(X)] = 0.25                       # every tile on the fast step
+    assert np.array_equal(_with_env(env, lambda: dev.predict(X, OUT_MARGIN)),
+                          xgb_ref.predict(ref, X, output_margin=True))
+    # multiclass: 3 groups of depth-8 trees, LW = 1 (tree_group per tree)
+    trees3, ti3 = xf.synthetic_complete_trees(27, 8, 28, seed=43, num_class=3)
+    f3 = xf.forest_from_raw_trees(trees3, ti3, 28, 3, 0.5, "multi:softprob")
+    r3 = xgb_ref.from_raw_trees(trees3, ti3, 28, 3, 0.5, "multi:softprob")
+    d3 = _with_env(env, lambda: DeviceForest(f3, [0]))
+    assert d3.info()["walk"] == 1
+    X = _edge_rows(trees3, 8, 28, 2049, seed=11)
+    assert np.array_equal(_with_env(env, lambda: d3.predict(X, OUT_MARGIN)),
+                          xgb_ref.predict(r3, X, output_margin=True))
+    np.testing.assert_allclose(_with_env(env, lambda: d3.predict(X, OUT_PREDICT)),
+                               xgb_ref.predict(r3, X), rtol=1e-5, atol=0)
+    # leaf ids keep the indexed walk
+    assert np.array_equal(dev.predict(X[:, :28], OUT_LEAF), xgb_ref.leaf_index(ref, X[:, :28]))

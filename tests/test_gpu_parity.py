@@ -327,6 +327,37 @@ def test_leafwise_lgb_full_property():
     assert np.array_equal(got, want)
 
 
+def test_leafwise_lgb_full_float64_specials():
+    """lgbserver's own dtype at C3 shape: the reference predicts a float64
+    DataFrame (python/lgbserver/lgbserver/model.py:46-51), so C3 traffic runs
+    the float64 bin view.  1000 trees x 255 leaves, 100 features, 250k float64
+    rows with NaN, +-0, 1e-36 / -1e-36 (LightGBM's |x| <= 1e-35 zero map),
+    1e-35 itself and values that differ from a threshold only past float32
+    precision, on the default layout (9): raw scores bit-exact against the C
+    restatement, probabilities within 1e-5."""
+    trees = lf.synthetic_leafwise_trees(1000, 255, 100, seed=1)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, 100, "binary sigmoid:1")
+        f = load_lightgbm_model(p)
+    dev = DeviceForest(f, [0])
+    assert dev.info()["layout"] == LAYOUT_ID["texplicit"]
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((250_000, 100))
+    thr = np.concatenate([t["threshold"] for t in trees])
+    pick = rng.random(X.shape)
+    at = thr[rng.integers(0, len(thr), X.shape)]
+    X = np.where(pick < 0.05, at, X)                                  # exactly at a threshold
+    X = np.where((pick >= 0.05) & (pick < 0.08), at + np.abs(at) * 1e-12, X)   # float64-only gap
+    sp = np.array([np.nan, 0.0, -0.0, 1e-36, -1e-36, 1e-35, 2e-35])
+    m = rng.random(X.shape) < 0.02
+    X[m] = sp[rng.integers(0, len(sp), m.sum())]
+    want = port.lgb_predict_raw(trees, 1, 100, X)[:, 0]
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), want)
+    np.testing.assert_allclose(dev.predict(X[:20_000], OUT_PREDICT),
+                               1.0 / (1.0 + np.exp(-want[:20_000])), rtol=RTOL)
+
+
 # ------------------------------------------------- every layout, same forest
 def _dev_with_layout(forest, layout):
     old = os.environ.get("TI_FORCE_LAYOUT")
@@ -340,14 +371,12 @@ def _dev_with_layout(forest, layout):
             os.environ["TI_FORCE_LAYOUT"] = old
 
 
-LAYOUT_ID = {"heap": 0, "explicit": 1, "compact": 2, "bheap": 3, "bexplicit": 4, "sexplicit": 5,
-             "rexplicit": 6, "lexplicit": 7, "hexplicit": 8,
-             "texplicit": 9}
+LAYOUT_ID = {"heap": 0, "explicit": 1, "bheap": 3, "rexplicit": 6, "lexplicit": 7,
+             "hexplicit": 8, "texplicit": 9}
 
 
-@pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit", "rexplicit", "lexplicit", "hexplicit",
-                                    "texplicit"])
+@pytest.mark.parametrize("layout", ["bheap", "heap", "explicit", "rexplicit", "lexplicit",
+                                    "hexplicit", "texplicit"])
 def test_xgb_golden_every_layout(golden, layout):
     g = np.load(os.path.join(golden, "xgb_synth.npz"))
     trees, ti = xf.synthetic_complete_trees(40, 8, 28, seed=1)
@@ -363,8 +392,8 @@ def test_xgb_golden_every_layout(golden, layout):
     np.testing.assert_allclose(dev3.predict(g["X"], OUT_PREDICT), g["prob3"], rtol=RTOL)
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit",
-                                    "lexplicit", "hexplicit", "texplicit"])
+@pytest.mark.parametrize("layout", ["explicit", "rexplicit", "lexplicit", "hexplicit",
+                                    "texplicit"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
     g = np.load(os.path.join(golden, "lgb_synth.npz"))
@@ -381,9 +410,8 @@ def test_lgb_golden_every_layout(golden, tmp_path, layout, dtype):
     assert np.array_equal(dev.predict(X, OUT_LEAF), lgb_ref.leaf_index(lm, Xd))
 
 
-@pytest.mark.parametrize("layout", ["bheap", "heap", "compact", "explicit", "bexplicit",
-                                    "sexplicit", "rexplicit", "lexplicit", "hexplicit",
-                                    "texplicit"])
+@pytest.mark.parametrize("layout", ["bheap", "heap", "explicit", "rexplicit", "lexplicit",
+                                    "hexplicit", "texplicit"])
 def test_lgb_iris_fixture_every_layout(golden, layout):
     from sklearn.datasets import load_iris
     path = os.path.join(golden, "lgb_iris_v3.txt")
@@ -393,46 +421,23 @@ def test_lgb_iris_fixture_every_layout(golden, layout):
     assert np.array_equal(dev.predict(X, OUT_MARGIN), lgb_ref.predict(m, X, raw_score=True))
 
 
-@pytest.mark.parametrize("layout", ["compact", "explicit", "bexplicit", "sexplicit", "rexplicit",
-                                    "lexplicit", "hexplicit", "texplicit"])
+@pytest.mark.parametrize("layout", ["explicit", "rexplicit", "lexplicit", "hexplicit",
+                                    "texplicit"])
 def test_sklearn_classifier_every_layout(golden, layout):
     fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
     gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
     dev = _dev_with_layout(fc, layout)
-    if dev.info()["layout"] != LAYOUT_ID[layout]:
-        pytest.skip("trees too large for the compact layout")
+    assert dev.info()["layout"] == LAYOUT_ID[layout]
     assert np.array_equal(dev.predict(gc["X"], OUT_MARGIN), gc["predict_proba"])
     assert np.array_equal(dev.predict(gc["X"], OUT_LEAF), gc["apply"])
 
 
-@pytest.mark.parametrize("rows", [1, 127, 129, 1000])
-def test_compact_ragged_and_specials(rows):
-    trees = lf.synthetic_leafwise_trees(37, 255, 40, seed=5)
-    with tempfile.TemporaryDirectory() as d:
-        p = os.path.join(d, "model.txt")
-        lf.write_lightgbm_text(p, trees, 40, "binary sigmoid:1")
-        f = load_lightgbm_model(p)
-    dev = _dev_with_layout(f, "compact")
-    assert dev.info()["layout"] == 2
-    rng = np.random.default_rng(rows)
-    X = rng.standard_normal((rows, 40))
-    sp = np.array([np.nan, 0.0, -0.0, 1e-40, np.inf, -np.inf])
-    mask = rng.random(X.shape) < 0.1
-    X[mask] = sp[rng.integers(0, len(sp), mask.sum())]
-    want = port.lgb_predict_raw(trees, 1, 40, X)[:, 0]
-    assert np.array_equal(dev.predict(X, OUT_MARGIN), want)
-    X32 = X.astype(np.float32)
-    assert np.array_equal(dev.predict(X32, OUT_MARGIN),
-                          port.lgb_predict_raw(trees, 1, 40, X32.astype(np.float64))[:, 0])
-
-
-@pytest.mark.parametrize("layout", ["bexplicit", "sexplicit", "rexplicit", "lexplicit", "hexplicit",
-                                    "texplicit"])
+@pytest.mark.parametrize("layout", ["rexplicit", "lexplicit", "hexplicit", "texplicit"])
 @pytest.mark.parametrize("rows", [1, 255, 257, 3000])
-def test_bexplicit_zero_missing_and_specials(rows, layout):
-    """Binned explicit kernels (nodes in global memory / staged in LDS) on
-    leaf-wise trees with every missing type: the zero rule runs on a dedicated
-    bin of exact 0 (after the |x| <= 1e-35 map)."""
+def test_record_zero_missing_and_specials(rows, layout):
+    """The record layouts (nodes gathered from global memory / staged in LDS)
+    on leaf-wise trees with every missing type: the zero rule runs on a
+    dedicated bin of exact 0 (after the |x| <= 1e-35 map)."""
     trees = lf.synthetic_leafwise_trees(41, 255, 40, seed=7)
     with tempfile.TemporaryDirectory() as d:
         p = os.path.join(d, "model.txt")

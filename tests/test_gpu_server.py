@@ -87,3 +87,53 @@ def test_lgbserver_inputs_batched_gpu(golden, tmp_path):
                                    rtol=1e-5, atol=0)
         assert np.array_equal(np.argmax(b["predictions"], axis=1),
                               np.argmax(lgb_ref.predict(m, X), axis=1))
+
+
+def test_c1_iris_32_single_row_requests_one_batch(golden, tmp_path):
+    """BASELINE config C1 as named: 32 concurrent single-row Iris v1 :predict
+    requests through xgbserver (the reference's legacy 0.82 fixture) with
+    --max_batchsize 32 are answered from ONE batch (one batchId:
+    test/e2e/batcher/test_batcher.py:71-78), and every answer is the
+    oracle's label for its row -- the reference's known answers among them
+    (X[0] -> 0, xgbserver/test_model.py:42-44; the e2e rows -> 1,
+    test/e2e/predictor/test_xgboost.py:67-68)."""
+    import threading
+    from sklearn.datasets import load_iris
+    from kfserving_amd.xgbserver import XGBoostModel, XGBoostModelRepository
+    from oracle import xgb_ref
+    path = _dir(golden, tmp_path, "xgb_iris_legacy_082.bst", "model.bst")
+    model = XGBoostModel("xgboost-iris", path, 1)
+    assert model.load()
+    server = KFServer(registered_models=XGBoostModelRepository(str(tmp_path)),
+                      max_batchsize=32, max_latency_ms=5000)
+    server.register_model(model)
+    s = _Running(server)
+    X = load_iris()["data"]
+    with open(os.path.join(golden, "iris_input.json")) as fh:
+        e2e = json.load(fh)["instances"]
+    rows = [X[0].tolist()] + e2e + [X[i].tolist() for i in range(5, 150, 5)][:29]
+    assert len(rows) == 32
+    ref = xgb_ref.read_xgb_binary(os.path.join(path, "model.bst"))
+    want = xgb_ref.predict(ref, np.asarray(rows, dtype=np.float32))
+    out = [None] * 32
+    start = threading.Barrier(32)
+
+    def one(i):
+        start.wait()
+        out[i] = s.fetch("/v1/models/xgboost-iris:predict", "POST",
+                         json.dumps({"instances": [rows[i]]}).encode())
+
+    th = [threading.Thread(target=one, args=(i,)) for i in range(32)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    s.stop()
+    bodies = []
+    for code, _, body in out:
+        assert code == 200
+        bodies.append(json.loads(body))
+    assert len({b["batchId"] for b in bodies}) == 1 and bodies[0]["batchId"]
+    got = [b["predictions"][0] for b in bodies]
+    assert got == [float(w) for w in want]
+    assert got[0] == 0 and got[1] == 1 and got[2] == 1        # the reference's known answers

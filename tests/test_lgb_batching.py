@@ -95,3 +95,16 @@ def test_lgb_inputs_batch_errors(golden, tmp_path):
     code, _, out = s.fetch("/v1/models/lightgbm:predict", "POST", b'{"inputs": 3}')
     assert code == 400
     s.stop()
+
+
+def test_lgb_matrix_mixed_bool_columns_follow_pandas():
+    """Columns pandas types as object (bool mixed with numbers, bool beside
+    None) take the pandas path and are rejected by lightgbm's dtype check;
+    all-bool and number + None columns are numeric."""
+    from kfserving_amd.tree_model import lgb_matrix_from_inputs
+    names = ["a", "b"]
+    for bad in ([True, 1], [True, None], [1, False]):
+        with pytest.raises(ValueError):
+            lgb_matrix_from_inputs([{"a": bad, "b": [1.0, 2.0]}], names)
+    X = lgb_matrix_from_inputs([{"a": [True, False], "b": [1, None]}], names)
+    np.testing.assert_array_equal(X, np.array([[1.0, 1.0], [0.0, np.nan]]))

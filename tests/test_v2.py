@@ -192,3 +192,23 @@ def test_v2_decode_units():
     assert v2.feature_matrix([("c", np.int64([1, 2]))]).dtype == np.float64
     assert not v2.is_tensor_request({"inputs": [{"a": [1]}]})      # lgbserver rows stay v1
     assert v2.is_tensor_request({"inputs": [{"name": "x", "shape": [1], "datatype": "FP32"}]})
+
+
+def test_v2_decode_errors_are_v2_errors():
+    """Every malformed tensor is a V2Error (400), never an escaping numpy
+    error: out-of-range integers, a non-int binary size, a bool
+    shape entry, a shape whose product overflows int64."""
+    cases = [
+        ({"inputs": [{"name": "x", "shape": [1], "datatype": "UINT8", "data": [-1]}]}, b""),
+        ({"inputs": [{"name": "x", "shape": [1], "datatype": "INT8", "data": [1000]}]}, b""),
+        ({"inputs": [{"name": "x", "shape": [2], "datatype": "FP32",
+                      "parameters": {"binary_data_size": 8.0}}]}, b"\0" * 8),
+        ({"inputs": [{"name": "x", "shape": [2], "datatype": "FP32",
+                      "parameters": {"binary_data_size": True}}]}, b"\0" * 8),
+        ({"inputs": [{"name": "x", "shape": [True], "datatype": "FP32", "data": [1.0]}]}, b""),
+        ({"inputs": [{"name": "x", "shape": [1 << 40, 1 << 40], "datatype": "FP32",
+                      "data": [1.0]}]}, b""),
+    ]
+    for req, tail in cases:
+        with pytest.raises(v2.V2Error):
+            v2.decode_inputs(req, tail)
