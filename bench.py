@@ -27,11 +27,13 @@ Also reported (rank 0):
   cpu_baseline -- the C/OpenMP restatement of xgboost 0.82's predict loop
                   (oracle/c/tree_port.c, kind "port": xgboost is not installed)
                   timed on this host on a bounded sample of the same rows.
-  c3, c3_f64, c4 -- the other named GPU configs at their BASELINE sizes, row-
-                  sharded over the ranks (strong scaling, max-over-ranks wall):
-                  C3 LightGBM leaf-wise 1000 x 255 leaves, F = 100, 100M rows,
-                  float32 X (c3) and float64 X (c3_f64: what lgbserver's
-                  DataFrame path feeds, lgbserver/model.py:46-51); C4 sklearn
+  c3, c3_f64, c3_maxbin, c4 -- the other named GPU configs at their BASELINE
+                  sizes, row-sharded over the ranks (strong scaling, max-over-
+                  ranks wall): C3 LightGBM leaf-wise 1000 x 255 leaves, F = 100,
+                  100M rows, float32 X (c3) and float64 X (c3_f64: what
+                  lgbserver's DataFrame path feeds, lgbserver/model.py:46-51);
+                  c3_maxbin the same shape as a max_bin-255 LightGBM model
+                  (quantile-edge thresholds: u8 bins); C4 sklearn
                   RandomForestRegressor 200 x depth 16, F = 64, 10M rows (the
                   cached fit of scripts/make_c4_model.py).  Each carries a
                   `roofline` (config_roofline): the busiest of VALU issue, LDS
@@ -79,7 +81,7 @@ def parse_args(argv=None):
     p.add_argument("--latency-qps", type=float, default=10000.0,
                    help="offered requests/s for the batched-latency leg (0 = skip)")
     p.add_argument("--latency-seconds", type=float, default=3.0)
-    p.add_argument("--configs", default="c3,c3_f64,c4",
+    p.add_argument("--configs", default="c3,c3_f64,c3_maxbin,c4",
                    help="other named configs to time after the headline ('' = none)")
     p.add_argument("--rows3", type=int, default=100_000_000)
     p.add_argument("--rows4", type=int, default=10_000_000)
@@ -393,14 +395,30 @@ def device_normal(rows, cols, seed, device, dtype="float32"):
     return X
 
 
-def c3_forest():
+def _lgb_forest(trees, what):
     import tempfile
     from kfserving_amd.formats import lightgbm_format as lf
-    trees = lf.synthetic_leafwise_trees(1000, 255, 100, seed=1)
     with tempfile.TemporaryDirectory() as d:
         p = os.path.join(d, "model.txt")
         lf.write_lightgbm_text(p, trees, 100, "binary sigmoid:1")
-        return lf.load_lightgbm_model(p), trees, "LightGBM text v3, seeded leaf-wise generator"
+        return lf.load_lightgbm_model(p), trees, what
+
+
+def c3_forest():
+    from kfserving_amd.formats import lightgbm_format as lf
+    return _lgb_forest(lf.synthetic_leafwise_trees(1000, 255, 100, seed=1),
+                       "LightGBM text v3, seeded leaf-wise generator (i.i.d. N(0,1) thresholds)")
+
+
+def c3_maxbin_forest():
+    """C3 shaped like a LightGBM model trained at max_bin = 255 on N(0,1)
+    features (lightgbm_format.synthetic_maxbin_trees): thresholds on the 254
+    quantile bin edges, intervals nested along each path, missing type None.
+    At most 254 thresholds a feature, so layout 9 bins to u8."""
+    from kfserving_amd.formats import lightgbm_format as lf
+    return _lgb_forest(lf.synthetic_maxbin_trees(1000, 255, 100, seed=1),
+                       "LightGBM text v3, seeded max_bin-255 leaf-wise generator "
+                       "(quantile-edge thresholds, nested intervals, missing type None)")
 
 
 def c4_forest():
@@ -451,6 +469,7 @@ def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_
                "steps": args.config_steps, "rows_per_s": total_rows * args.config_steps / wall,
                "ms_per_step": wall / args.config_steps * 1e3, "kernel_ms_rank0": kms,
                "layout": LAYOUT_NAMES.get(eng.info()["layout"]),
+               "bin_bits": eng.info().get("bin_bits"),
                "compulsory_GBps": ((X.element_size() * n_feat + out.element_size()) * rows
                                    / (kms * 1e-3) / 1e9 if kms else None)}
         if pmc_path and kms:
@@ -617,8 +636,8 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
 
     configs = {}
     for name in [c.strip() for c in args.configs.split(",") if c.strip()]:
-        if name in ("c3", "c3_f64"):
-            f3, t3, src = c3_forest()
+        if name in ("c3", "c3_f64", "c3_maxbin"):
+            f3, t3, src = c3_maxbin_forest() if name == "c3_maxbin" else c3_forest()
             dt = "float64" if name == "c3_f64" else "float32"
             r = run_config(f3, 100, args.rows3, 3, args, world, rank, device, dev_sync,
                            make_engine, c3_cpu(t3, args.cpu_seconds / 2, dt), name,

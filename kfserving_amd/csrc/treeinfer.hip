@@ -481,6 +481,7 @@ struct ti_forest {
     int32_t rows = 256;
     int32_t words = 0;
     int32_t kary = 0;            // > 0: tbl holds 5-ary search tables of this height
+    int32_t b8 = 0;              // u8 bins (layout 9 only; RxBins<true> in the kernels)
     std::vector<uint32_t> top;   // heap tops (layout 8): [T][2^(hx_top+1)] u32
   } rx[2];
   std::vector<uint32_t> h_rx_base, h_rx_nint;   // h_rx_base: [T+1]
@@ -1026,18 +1027,28 @@ bool plan_rx_slots(const ti_forest_desc* d, ti_forest* f, std::vector<uint32_t>*
 // Records of one input view (ranks differ between the float32 and float64
 // views).  Returns false when the bins do not fit u16 (more than 65,533
 // distinct thresholds on a feature; 16,382 for zero-missing forests, whose
-// bins are doubled) or the bin image does not fit 64 KB at 64-row tiles.
+// bins are doubled) or, with b8, u8 (254; 126 with the zero rule: NaN is bin
+// 0, values 1 .. m + 1), or the bin image does not fit 64 KB at 64-row tiles.
+// u8 images hold four bins a word, so a tile of twice the rows (512,
+// TI_RX_ROWS8) fits the LDS a u16 tile of 256 takes: 4 waves per SIMD
+// instead of 2 at C3's 100 features.
 template <typename XT, typename ACC>
 bool pack_rexplicit(const ti_forest_desc* d, const ti_forest* f,
-                    const std::vector<uint32_t>& slot_of, ti_forest::RecExplicit* rx) {
+                    const std::vector<uint32_t>& slot_of, ti_forest::RecExplicit* rx,
+                    bool b8 = false) {
   const bool zero = f->zero_rule != 0;
   const RankTables<XT> rt = collect_ranks<XT>(d, zero);
-  if (rt.m_max > (zero ? 16382u : 65533u)) return false;
-  rx->words = (d->n_features + 1) / 2;
+  if (rt.m_max > (b8 ? (zero ? 126u : 254u) : (zero ? 16382u : 65533u))) return false;
+  const int P = b8 ? 4 : 2;   // bins per word
+  rx->b8 = b8 ? 1 : 0;
+  rx->words = (d->n_features + P - 1) / P;
+  const uint32_t nan_left = b8 ? ti::RxBins<true>::kNanLeft : ti::kRxNanLeft;
+  const uint32_t zero_flip = b8 ? ti::RxBins<true>::kZeroFlip : ti::kRxZeroFlip;
   // a power of two in [64, 512]: the kernels OR the lane part (tid * 4) into
   // the feature's word offset (word * R * 4), which holds only then
   int R = 64;
-  while (R < 512 && 2 * R <= env_int("TI_RX_ROWS", 256)) R *= 2;
+  const int want_rows = b8 ? env_int("TI_RX_ROWS8", 512) : env_int("TI_RX_ROWS", 256);
+  while (R < 512 && 2 * R <= want_rows) R *= 2;
   while (R > 64 && static_cast<size_t>(rx->words) * R * 4 > kFeatLdsMax) R >>= 1;
   if (static_cast<size_t>(rx->words) * R * 4 > kFeatLdsMax) return false;
   rx->rows = R;
@@ -1063,12 +1074,12 @@ bool pack_rexplicit(const ti_forest_desc* d, const ti_forest* f,
         }
       } else {
         const int fe = d->feature[g];
-        const uint32_t off = static_cast<uint32_t>((fe / 2) * R * 4 + (fe % 2) * 2);
+        const uint32_t off = static_cast<uint32_t>((fe / P) * R * 4 + (fe % P) * (4 / P));
         const uint32_t rank = rt.rank(fe, d->threshold[g]);
-        r.x = off | ((d->flags[g] & TI_NODE_NAN_LEFT) ? ti::kRxNanLeft : 0u);
+        r.x = off | ((d->flags[g] & TI_NODE_NAN_LEFT) ? nan_left : 0u);
         if (zero) {
           r.x |= (2u * rank + 1u) << 16;   // <= 32,765: bit 31 stays clear
-          if (d->flags[g] & TI_NODE_ZERO_FLIP) r.x |= ti::kRxZeroFlip;
+          if (d->flags[g] & TI_NODE_ZERO_FLIP) r.x |= zero_flip;
         } else {
           r.x |= rank << 16;
         }
@@ -1141,6 +1152,7 @@ bool plan_lx_stages(ti_forest* f, int T) {
 // [2^D0, 2^(D0+1)) the layout-6 slot where the walk continues: the node at
 // depth D0, or the leaf that ended the path above it.
 constexpr uint32_t kHxPad = 0xFFFF0000u | ti::kRxNanLeft;
+constexpr uint32_t kHxPad8 = 0xFFFF0000u | ti::RxBins<true>::kNanLeft;   // u8 bins (layout 9)
 constexpr int kHxPf = 8;   // = PF of hexplicit_predict_kernel
 void pack_htop(const ti_forest_desc* d, const std::vector<uint32_t>& slot_of, int D0,
                ti_forest::RecExplicit* rx) {
@@ -1288,7 +1300,7 @@ bool plan_tx(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>&
           continue;
         }
         const bool leaf = d->feature[g] < 0;
-        top[it.p] = leaf ? kHxPad : rx.recs[b + slot_of[g]].x;
+        top[it.p] = leaf ? (rx.b8 ? kHxPad8 : kHxPad) : rx.recs[b + slot_of[g]].x;
         st.push_back(Item{leaf ? it.v : d->left[g], 2 * it.p, it.l + 1});
         st.push_back(Item{leaf ? it.v : d->right[g], 2 * it.p + 1, it.l + 1});
       }
@@ -1575,11 +1587,11 @@ int32_t bin_chunk_for(size_t bytes, int R, int xdt, int F) {
   return c >= 8 ? static_cast<int32_t>(c) : 0;
 }
 
-KernelFn select_texplicit(int xdt, int accum, int K, bool z, int ilp) {
-  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(9, K, true, z, true, ilp);
-  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(9, K, true, z, true, ilp);
-  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(9, K, true, z, true, ilp);
-  return ti::kernels_df(9, K, true, z, true, ilp);
+KernelFn select_texplicit(int xdt, int accum, int K, bool z, int ilp, bool b8) {
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(9, K, true, z, !b8, ilp);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(9, K, true, z, !b8, ilp);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(9, K, true, z, !b8, ilp);
+  return ti::kernels_df(9, K, true, z, !b8, ilp);
 }
 
 KernelFn select_hexplicit(int xdt, int accum, int K, bool z, int ilp) {
@@ -1847,7 +1859,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (lds > kLdsPerCu || static_cast<int64_t>(kLxPf) * 16 * R < f->lx_stage_cap)
       return fail(TI_ERR_UNSUPPORTED, "heap-top staged layout exceeds LDS");
     a.bin_chunk = bin_chunk_for(static_cast<size_t>(f->lx_stage_cap), R, xdt, f->F);
-    KernelFn fn = select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp);
+    KernelFn fn = select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp, rx.b8 != 0);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -2574,12 +2586,20 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         env_int("TI_NO_REXPLICIT", 0) == 0) {
       std::vector<uint32_t> slot_of;
       rx_ok = plan_rx_slots(desc, f.get(), &slot_of);
-      if (rx_ok && f->accum == TI_F64)
-        rx_ok = pack_rexplicit<float, double>(desc, f.get(), slot_of, &f->rx[0]) &&
-                pack_rexplicit<double, double>(desc, f.get(), slot_of, &f->rx[1]);
-      else if (rx_ok)
-        rx_ok = pack_rexplicit<float, float>(desc, f.get(), slot_of, &f->rx[0]) &&
-                pack_rexplicit<double, float>(desc, f.get(), slot_of, &f->rx[1]);
+      auto pack_views = [&](bool b8) {
+        if (f->accum == TI_F64)
+          return pack_rexplicit<float, double>(desc, f.get(), slot_of, &f->rx[0], b8) &&
+                 pack_rexplicit<double, double>(desc, f.get(), slot_of, &f->rx[1], b8);
+        return pack_rexplicit<float, float>(desc, f.get(), slot_of, &f->rx[0], b8) &&
+               pack_rexplicit<double, float>(desc, f.get(), slot_of, &f->rx[1], b8);
+      };
+      // u8 bins where every feature's thresholds fit them and layout 9 takes
+      // the forest (only layout 9 reads u8 images; TI_RX_B8=0 keeps u16)
+      const bool try8 = rx_ok && env_int("TI_RX_B8", 1) != 0 &&
+                        (want.empty() || want == "texplicit") &&
+                        env_int("TI_NO_TEXPLICIT", 0) == 0;
+      bool b8 = try8 && pack_views(true) && plan_tx(desc, f.get(), slot_of, D);
+      if (!b8 && rx_ok) rx_ok = pack_views(false);
       if (rx_ok) {
         f->layout = 6;
         // trees in flight per lane: 16 for shallow-on-average forests (C3,
@@ -2594,8 +2614,10 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         // (layout 7, forced or TI_NO_TEXPLICIT=1); deep trees too large for a
         // stage: heap tops in LDS, the rest gathered (layout 8)
         const bool auto_ok = want != "rexplicit" && want != "hexplicit" && want != "lexplicit";
-        if ((want == "texplicit" || (auto_ok && env_int("TI_NO_TEXPLICIT", 0) == 0)) &&
-            plan_tx(desc, f.get(), slot_of, D)) {
+        if (b8) {
+          f->layout = 9;   // u8 bins (planned above)
+        } else if ((want == "texplicit" || (auto_ok && env_int("TI_NO_TEXPLICIT", 0) == 0)) &&
+                   plan_tx(desc, f.get(), slot_of, D)) {
           // layout 9
         } else if ((want == "lexplicit" || auto_ok) && env_int("TI_NO_LEXPLICIT", 0) == 0 &&
                    plan_lx_stages(f.get(), f->T)) {
@@ -2676,7 +2698,8 @@ int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
   }
   info->tree_stride_bytes = f->layout == 0 ? f->stride32 : f->layout == 3 ? f->bh[0].stride : 0;
   info->walk = bheap_fixed(f, TI_F32, TI_OUTPUT_PREDICT) ? 1 : 0;
-  info->bin_bits = f->layout == 3 ? (f->bh[0].b16 ? 16 : 8) : 0;
+  info->bin_bits = f->layout == 3 ? (f->bh[0].b16 ? 16 : 8)
+                   : (f->layout >= 6 && f->layout <= 9) ? (f->rx[0].b8 ? 8 : 16) : 0;
   return TI_OK;
 }
 

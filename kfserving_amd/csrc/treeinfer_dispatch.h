@@ -14,19 +14,25 @@ using KernelFn = void (*)(KArgs);
 // bottom (2, 4 and 5 were retired in round 3); 10 selects the fixed-layout
 // walk of layout 3 (bheap_fix_kernel).
 // fl: feature image in
-// LDS; z: LightGBM zero rule; b16 / pf: binned heap bin width and prefetch
-// depth.
+// LDS; z: LightGBM zero rule; b16 / pf: binned heap (and layout 9) bin width
+// and prefetch depth.
+template <typename XT, typename ACC, int KMAX, bool B8>
+KernelFn select_tx(bool z, int pf) {
+  if constexpr (sizeof(ACC) == 8) {
+    if (z) return pf >= 8 ? texplicit_predict_kernel<XT, ACC, KMAX, true, 8, B8>
+                  : pf == 7 ? texplicit_predict_kernel<XT, ACC, KMAX, true, 7, B8>
+                            : texplicit_predict_kernel<XT, ACC, KMAX, true, 4, B8>;
+  }
+  return pf >= 8 ? texplicit_predict_kernel<XT, ACC, KMAX, false, 8, B8>
+         : pf == 7 ? texplicit_predict_kernel<XT, ACC, KMAX, false, 7, B8>
+                   : texplicit_predict_kernel<XT, ACC, KMAX, false, 4, B8>;
+}
+
 template <typename XT, typename ACC, int KMAX>
 KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
-  if (layout == 9) {   // pf carries the tree ILP (4, 7 or 8)
-    if constexpr (sizeof(ACC) == 8) {
-      if (z) return pf >= 8 ? texplicit_predict_kernel<XT, ACC, KMAX, true, 8>
-                    : pf == 7 ? texplicit_predict_kernel<XT, ACC, KMAX, true, 7>
-                              : texplicit_predict_kernel<XT, ACC, KMAX, true, 4>;
-    }
-    return pf >= 8 ? texplicit_predict_kernel<XT, ACC, KMAX, false, 8>
-           : pf == 7 ? texplicit_predict_kernel<XT, ACC, KMAX, false, 7>
-                     : texplicit_predict_kernel<XT, ACC, KMAX, false, 4>;
+  if (layout == 9) {   // pf carries the tree ILP (4, 7 or 8); b16 false: u8 bins
+    if (!b16) return select_tx<XT, ACC, KMAX, true>(z, pf);
+    return select_tx<XT, ACC, KMAX, false>(z, pf);
   }
   if (layout == 8) {   // pf carries the tree ILP (4 or 8)
     if constexpr (sizeof(ACC) == 8) {

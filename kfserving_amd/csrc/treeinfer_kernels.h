@@ -1095,6 +1095,22 @@ __global__ void __launch_bounds__(512) explicit_predict_kernel(const KArgs a) {
 constexpr uint32_t kRxNanLeft = 1u;
 constexpr uint32_t kRxZeroFlip = 4u;
 constexpr uint32_t kRxOffMask = 0xFFFAu;   // the bin byte offset without the flag bits
+// u8 bins (layout 9 when every feature has <= 254 distinct thresholds, <= 126
+// with the zero rule; lightgbm max_bin = 255 models): four features per word,
+// so the byte offset keeps bits 0-1 and the flags move into the lane part
+// (bits 2 and 3, cleared before the lane offset is OR-ed in).  NaN is bin 0
+// (the bins of values are 1 .. m + 1), which the rank compare sends left; a
+// tile holding a NaN takes the slow step, which tests b == 0 first.
+template <bool B8> struct RxBins {
+  static constexpr uint32_t kNanLeft = 1u, kZeroFlip = 4u, kOffMask = 0xFFFAu;
+  template <bool ZERO> static constexpr uint32_t nan_code() { return ZERO ? 0xFFFEu : 0xFFFFu; }
+  static constexpr int kPerWord = 2;
+};
+template <> struct RxBins<true> {
+  static constexpr uint32_t kNanLeft = 4u, kZeroFlip = 8u, kOffMask = 0xFFF3u;
+  template <bool ZERO> static constexpr uint32_t nan_code() { return 0u; }
+  static constexpr int kPerWord = 4;
+};
 
 // Slot loads are structured buffer loads: vindex = the slot (VGPR), soffset =
 // the tree's first byte (wave-uniform SGPR), stride 8 in the resource, so the
@@ -1128,22 +1144,31 @@ __device__ __forceinline__ uint32_t rx_next_fast(uint32_t x, uint32_t y, uint16_
       : "=v"(slot) : "v"(x), "v"(y), "v"(b) : "vcc");
   return slot;
 }
-template <bool ZERO>
+template <bool ZERO, bool B8 = false>
 __device__ __forceinline__ uint32_t rx_next_slow(uint32_t x, uint32_t y, uint16_t b16) {
-  constexpr uint32_t kNan = ZERO ? 0xFFFEu : 0xFFFFu;
+  using W = RxBins<B8>;
+  constexpr uint32_t kNan = W::template nan_code<ZERO>();
   const uint32_t b = b16;
   bool right = (x >> 16) < b;
-  if (ZERO) right = right != (((b & 1u) != 0u) && ((x & kRxZeroFlip) != 0u));
-  if (b == kNan) right = (x & kRxNanLeft) == 0u;
+  if (ZERO) right = right != (((b & 1u) != 0u) && ((x & W::kZeroFlip) != 0u));
+  if (b == kNan) right = (x & W::kNanLeft) == 0u;
   return right ? (y >> 16) : (y & 0xFFFFu);
 }
-template <bool ZERO, bool SLOW>
+template <bool ZERO, bool SLOW, bool B8 = false>
 __device__ __forceinline__ uint32_t rx_next(uint32_t x, uint32_t y, uint16_t b) {
-  return SLOW ? rx_next_slow<ZERO>(x, y, b) : rx_next_fast(x, y, b);
+  return SLOW ? rx_next_slow<ZERO, B8>(x, y, b) : rx_next_fast(x, y, b);
 }
 __device__ __forceinline__ uint16_t lds_u16(uint32_t byte_addr) {
   return *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(
       static_cast<uintptr_t>(byte_addr));
+}
+__device__ __forceinline__ uint16_t lds_u8(uint32_t byte_addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(
+      static_cast<uintptr_t>(byte_addr));
+}
+template <bool B8>
+__device__ __forceinline__ uint16_t lds_rxbin(uint32_t byte_addr) {
+  return B8 ? lds_u8(byte_addr) : lds_u16(byte_addr);
 }
 
 // Bin the tile's rows (one lane per row, per-lane loads)
@@ -1162,7 +1187,7 @@ __device__ __forceinline__ uint16_t lds_u16(uint32_t byte_addr) {
 // Search Q consecutive features [f0, f0 + Q) of the lane's row (values x,
 // NaN past the last feature) and store their packed u16 bins in the image
 // (f0 even).  With ZB (zero-missing forests) b2 = 2 b + (x == 0), NaN 0xFFFE.
-template <typename XT, bool ZB, bool KARY, int Q, bool SROOT = false>
+template <typename XT, bool ZB, bool KARY, int Q, bool SROOT = false, bool B8 = false>
 __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], int f0, int R, int tid,
                                              bool& has_nan) {
   const int F = a.n_features;
@@ -1222,22 +1247,24 @@ __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], i
       for (int q = 0; q < Q; ++q) k[q] = 2u * k[q] + (e[q] < x[q] ? 1u : 0u);
     }
   }
-  uint32_t w[Q / 2];
+  constexpr int P = RxBins<B8>::kPerWord;   // bins per 32-bit word (f0 % P == 0)
+  constexpr uint32_t kNan = RxBins<B8>::template nan_code<ZB>();
+  uint32_t w[Q / P];
 #pragma unroll
-  for (int j = 0; j < Q / 2; ++j) w[j] = 0u;
+  for (int j = 0; j < Q / P; ++j) w[j] = 0u;
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const bool nan = x[q] != x[q];
     const bool zero = ZB && x[q] == XT(0);
     has_nan |= (nan || zero) && (f0 + q < F);   // the tile needs the slow step
     uint32_t b = 1u + k[q] - tsz;
-    if (ZB) b = nan ? 0xFFFEu : 2u * b + (zero ? 1u : 0u);
-    else b = nan ? 0xFFFFu : b;
-    w[q / 2] |= b << ((q % 2) * 16);
+    if (ZB) b = nan ? kNan : 2u * b + (zero ? 1u : 0u);
+    else b = nan ? kNan : b;
+    w[q / P] |= b << ((q % P) * (32 / P));
   }
 #pragma unroll
-  for (int j = 0; j < Q / 2; ++j) {
-    const int word = f0 / 2 + j;
+  for (int j = 0; j < Q / P; ++j) {
+    const int word = f0 / P + j;
     if (word < a.bin_words) {
       __attribute__((address_space(3))) uint32_t* dst =
           reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
@@ -1256,7 +1283,7 @@ __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], i
 // lines: C3's 400-byte rows made that 0.57 ms of a 5.5 ms kernel).  Returns
 // (uniformly) whether the tile needs the slow step: a NaN, or with ZB an
 // exact 0.
-template <typename XT, bool ZB, bool KARY = false, bool SROOT = false>
+template <typename XT, bool ZB, bool KARY = false, bool SROOT = false, bool B8 = false>
 __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp, const KArgs& a,
                                                    int64_t row0, int R, int tid) {
   constexpr int Q = TI_RX_BINQ;
@@ -1290,7 +1317,7 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
         XT x[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) x[q] = c + q < kc ? temp[(c + q) * R + tid] : nan_value<XT>();
-        rx_bin_group<XT, ZB, KARY, Q, SROOT>(a, x, f0 + c, R, tid, has_nan);
+        rx_bin_group<XT, ZB, KARY, Q, SROOT, B8>(a, x, f0 + c, R, tid, has_nan);
       }
     }
   } else {
@@ -1302,7 +1329,7 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
         const int f = f0 + q < F ? f0 + q : F - 1;
         x[q] = f0 + q < FC ? zero_map(xr[f], a.lgb_zero_map) : nan_value<XT>();
       }
-      rx_bin_group<XT, ZB, KARY, Q, SROOT>(a, x, f0, R, tid, has_nan);
+      rx_bin_group<XT, ZB, KARY, Q, SROOT, B8>(a, x, f0, R, tid, has_nan);
     }
   }
   __syncthreads();   // flag = 0 is visible before any lane sets it
@@ -1315,14 +1342,15 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
 // (a.bin_kary > 0), every other view the Eytzinger tables.
 // SROOT: the 5-ary root as a scalar load (layout 8: C4 2.17 -> 2.13 ms; on
 // layout 9 it cost C3 0.7 %, profiles/r2_kary_root_sweep.jsonl)
-template <typename XT, bool ZB, bool SROOT = false>
+template <typename XT, bool ZB, bool SROOT = false, bool B8 = false>
 __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
                                               int R, int tid, void* temp = nullptr) {
   if constexpr (sizeof(XT) == 4) {
     if (a.bin_kary > 0)
-      return rx_stage_bins_impl<XT, ZB, true, SROOT>(flag, static_cast<XT*>(temp), a, row0, R, tid);
+      return rx_stage_bins_impl<XT, ZB, true, SROOT, B8>(flag, static_cast<XT*>(temp), a, row0, R,
+                                                         tid);
   }
-  return rx_stage_bins_impl<XT, ZB, false>(flag, static_cast<XT*>(temp), a, row0, R, tid);
+  return rx_stage_bins_impl<XT, ZB, false, false, B8>(flag, static_cast<XT*>(temp), a, row0, R, tid);
 }
 
 // Per step every tree's bin read is issued first, then each tree's decision
@@ -1366,8 +1394,9 @@ typedef const __attribute__((address_space(4))) uint32_t rx_cu32;   // scalar-lo
 // inside a tree, the lane's own column of word 0 at its leaf.  The empty asm keeps the
 // compiler from rewriting the select as and / cndmask / or: v_and_or_b32 and
 // one v_cndmask_b32, 2 VALU instead of 3.
+template <bool B8 = false>
 __device__ __forceinline__ uint32_t rx_bin_addr(uint32_t x, bool in, uint32_t lane_off) {
-  uint32_t t = (x & kRxOffMask) | lane_off;
+  uint32_t t = (x & RxBins<B8>::kOffMask) | lane_off;
 #if TI_RX_ADDR2
   asm("" : "+v"(t));
 #endif
@@ -1610,12 +1639,13 @@ __global__ void __launch_bounds__(512) lexplicit_predict_kernel(const KArgs a) {
 // LDS round trip per level, every lane busy at every level -- and the rest of
 // the tree by layout 6's exec-masked gathers from that slot.  Leaves are
 // added in tree order, so sums are layout 6's, bit for bit.
-template <bool ZERO>
+template <bool ZERO, bool B8 = false>
 __device__ __forceinline__ bool rx_right_slow(uint32_t x, uint32_t b) {
-  constexpr uint32_t kNan = ZERO ? 0xFFFEu : 0xFFFFu;
+  using W = RxBins<B8>;
+  constexpr uint32_t kNan = W::template nan_code<ZERO>();
   bool right = (x >> 16) < b;
-  if (ZERO) right = right != (((b & 1u) != 0u) && ((x & kRxZeroFlip) != 0u));
-  if (b == kNan) right = (x & kRxNanLeft) == 0u;
+  if (ZERO) right = right != (((b & 1u) != 0u) && ((x & W::kZeroFlip) != 0u));
+  if (b == kNan) right = (x & W::kNanLeft) == 0u;
   return right;
 }
 
@@ -1740,7 +1770,7 @@ __global__ void __launch_bounds__(512) hexplicit_predict_kernel(const KArgs a) {
 // group runs for its deepest path), then the bottom in layout 7's lockstep.
 // KArgs: trees = image, depth = D0, rx_base = byte offset of each tree in the
 // image [T+1], rx_nint = internal nodes of each bottom [T].
-template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP>
+template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP, bool B8>
 __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t0, int t1,
                                          uint32_t sbase, uint32_t lane_off, int64_t row,
                                          bool live) {
@@ -1764,7 +1794,7 @@ __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t
       rx_u2_t pr[ILP];
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
-        b[q] = lds_u16((nd[q] & kRxOffMask) | lane_off);
+        b[q] = lds_rxbin<B8>((nd[q] & RxBins<B8>::kOffMask) | lane_off);
         pr[q] = lx_rec(base[q] + 8u * idx[q]);
       }
 #pragma unroll
@@ -1776,7 +1806,7 @@ __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t
               : "+v"(nd[q]), "+v"(idx[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y)
               : "vcc");
         } else {
-          const bool right = rx_right_slow<ZERO>(nd[q], b[q]);
+          const bool right = rx_right_slow<ZERO, B8>(nd[q], b[q]);
           idx[q] = idx[q] + idx[q] + (uint32_t)right;
           nd[q] = right ? pr[q].y : pr[q].x;
         }
@@ -1797,11 +1827,11 @@ __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t
       for (int q = 0; q < ILP; ++q) {
         in[q] = at[q] < ni8[q];
         any |= in[q];
-        b[q] = lds_u16(rx_bin_addr(rec[q].x, in[q], lane_off));
+        b[q] = lds_rxbin<B8>(rx_bin_addr<B8>(rec[q].x, in[q], lane_off));
       }
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
-        const uint32_t nx = rx_next<ZERO, SLOW>(rec[q].x, rec[q].y, (uint16_t)b[q]);
+        const uint32_t nx = rx_next<ZERO, SLOW, B8>(rec[q].x, rec[q].y, (uint16_t)b[q]);
         at[q] = in[q] ? nx : at[q];
         rec[q] = lx_rec(base[q] + at[q]);
       }
@@ -1815,7 +1845,7 @@ __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t
   }
 }
 
-template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
+template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP, bool B8 = false>
 __global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int PF = 8;   // = kLxPf (host): a stage is at most PF x 16 B x R
@@ -1835,7 +1865,7 @@ __global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
   auto n16_of = [&](int s) { return (int)((tx_off[sst[s + 1]] - tx_off[sst[s]]) >> 4); };
   u32x4 pf[PF];
   prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(0)), n16_of(0), tid, R);
-  const bool slow = rx_stage_bins<XT, ZERO>(flag, a, row0, R, tid, stage);
+  const bool slow = rx_stage_bins<XT, ZERO, false, B8>(flag, a, row0, R, tid, stage);
   const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
   ACC acc[KMAX];
   init_acc(acc, a);
@@ -1849,11 +1879,11 @@ __global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
     prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(sn)), n16_of(sn), tid, R);
     const uint32_t sbase = (uint32_t)a.stage_off - lo;   // LDS address = sbase + image byte
     if (slow) {
-      if (vis) tx_stage<ACC, KMAX, ZERO, true, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
-      else tx_stage<ACC, KMAX, ZERO, true, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+      if (vis) tx_stage<ACC, KMAX, ZERO, true, true, ILP, B8>(a, acc, t0, t1, sbase, lane_off, row, live);
+      else tx_stage<ACC, KMAX, ZERO, true, false, ILP, B8>(a, acc, t0, t1, sbase, lane_off, row, live);
     } else {
-      if (vis) tx_stage<ACC, KMAX, ZERO, false, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
-      else tx_stage<ACC, KMAX, ZERO, false, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live);
+      if (vis) tx_stage<ACC, KMAX, ZERO, false, true, ILP, B8>(a, acc, t0, t1, sbase, lane_off, row, live);
+      else tx_stage<ACC, KMAX, ZERO, false, false, ILP, B8>(a, acc, t0, t1, sbase, lane_off, row, live);
     }
   }
   if (!live || a.kind == TI_OUTPUT_LEAF) return;

@@ -1,0 +1,114 @@
+"""Layout 9 with u8 bins (treeinfer_kernels.h RxBins<true>): forests whose
+features have at most 254 distinct thresholds (126 with LightGBM's zero rule)
+bin to one byte, four features a word, NaN as bin 0.  Every case is checked
+bit for bit against the C restatement of lightgbm 2.3.1's predict loop
+(oracle/c/tree_port.c) and against the u16 image of the same forest
+(TI_RX_B8=0), on float32 and float64 inputs, with NaN, +-0, LightGBM's
+|x| <= 1e-35 zero map, +-inf and values exactly at a threshold."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from kfserving_amd.engine import DeviceForest
+from kfserving_amd.forest import MISSING_NAN, MISSING_NONE, MISSING_ZERO, OUT_LEAF, OUT_MARGIN
+from kfserving_amd.formats import load_lightgbm_model
+from kfserving_amd.formats import lightgbm_format as lf
+from oracle import port
+
+pytestmark = pytest.mark.gpu
+
+TEXPLICIT = 9
+
+
+def _forest(trees, F):
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, F, "binary sigmoid:1")
+        return load_lightgbm_model(p)
+
+
+def _device(forest, monkeypatch, b8: bool):
+    monkeypatch.setenv("TI_RX_B8", "1" if b8 else "0")
+    dev = DeviceForest(forest, [0])
+    monkeypatch.delenv("TI_RX_B8")
+    return dev
+
+
+def _inputs(trees, rows, F, seed, special_frac=0.03, at_frac=0.05):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((rows, F))
+    thr = np.concatenate([np.asarray(t["threshold"], dtype=np.float64) for t in trees])
+    pick = rng.random(X.shape)
+    X = np.where(pick < at_frac, thr[rng.integers(0, len(thr), X.shape)], X)
+    sp = np.array([np.nan, 0.0, -0.0, 1e-36, -1e-40, 1e-35, 2e-35, np.inf, -np.inf])
+    m = rng.random(X.shape) < special_frac
+    X[m] = sp[rng.integers(0, len(sp), m.sum())]
+    return X
+
+
+@pytest.mark.parametrize("missing", ["none", "all"])
+def test_maxbin_u8_matches_port_and_u16(monkeypatch, missing):
+    mts = (MISSING_NONE,) if missing == "none" else (MISSING_NONE, MISSING_ZERO, MISSING_NAN)
+    # the zero rule doubles the bins (<= 126 thresholds) and adds {-denorm_min, 0}
+    # to every zero-missing feature's thresholds: 124 edges + 2
+    max_bin = 255 if missing == "none" else 125
+    trees = lf.synthetic_maxbin_trees(60, 255, 40, seed=3, max_bin=max_bin, missing_types=mts)
+    f = _forest(trees, 40)
+    d8 = _device(f, monkeypatch, True)
+    d16 = _device(f, monkeypatch, False)
+    assert d8.info()["layout"] == TEXPLICIT and d8.info()["bin_bits"] == 8
+    assert d16.info()["layout"] == TEXPLICIT and d16.info()["bin_bits"] == 16
+    X = _inputs(trees, 5003, 40, seed=11)
+    X[:1536][~np.isfinite(X[:1536])] = 0.25          # fast tiles first (512-row u8 tiles)
+    X[:1536][X[:1536] == 0] = 0.25
+    for Xi in (X, X.astype(np.float32)):
+        want = port.lgb_predict_raw(trees, 1, 40, Xi.astype(np.float64))[:, 0]
+        got = d8.predict(Xi, OUT_MARGIN)
+        assert np.array_equal(got, want)
+        assert np.array_equal(got, d16.predict(Xi, OUT_MARGIN))
+        assert np.array_equal(d8.predict(Xi, OUT_LEAF), d16.predict(Xi, OUT_LEAF))
+
+
+@pytest.mark.parametrize("rows", [1, 511, 513, 2048])
+def test_u8_ragged_tiles(monkeypatch, rows):
+    trees = lf.synthetic_maxbin_trees(30, 127, 24, seed=rows)
+    f = _forest(trees, 24)
+    d8 = _device(f, monkeypatch, True)
+    assert d8.info()["bin_bits"] == 8
+    X = _inputs(trees, rows, 24, seed=rows + 5)
+    want = port.lgb_predict_raw(trees, 1, 24, X)[:, 0]
+    assert np.array_equal(d8.predict(X, OUT_MARGIN), want)
+
+
+@pytest.mark.parametrize("n_trees,bits", [(20, 8), (40, 16)])
+def test_u8_limit(monkeypatch, n_trees, bits):
+    """At the u8 limit: 20 trees on max_bin-256 edges put 254 distinct
+    thresholds on a feature (bin 255 is reachable, NaN is 0), 40 trees put
+    255, which does not fit u8, so the forest keeps u16 bins.  Same answers."""
+    trees = lf.synthetic_maxbin_trees(n_trees, 255, 4, seed=1, max_bin=256)   # 255 bin edges
+    f = _forest(trees, 4)
+    counts = [len(np.unique(np.concatenate([np.asarray(t["threshold"])[np.asarray(
+        t["split_feature"]) == j] for t in trees]))) for j in range(4)]
+    assert max(counts) == (254 if bits == 8 else 255)
+    dev = _device(f, monkeypatch, True)
+    assert dev.info()["layout"] == TEXPLICIT and dev.info()["bin_bits"] == bits
+    X = _inputs(trees, 3000, 4, seed=2)
+    X[:, 0] = np.where(np.arange(3000) % 7 == 0, 9.0, X[:, 0])       # above every edge: top bin
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), port.lgb_predict_raw(trees, 1, 4, X)[:, 0])
+
+
+def test_c3_maxbin_full_float64():
+    """c3_maxbin at C3 shape (1000 trees x 255 leaves, 100 features): 200k
+    float64 rows, the dtype lgbserver feeds (lgbserver/model.py:46-51), bit
+    exact against the C restatement on layout 9 with u8 bins."""
+    trees = lf.synthetic_maxbin_trees(1000, 255, 100, seed=1)
+    dev = DeviceForest(_forest(trees, 100), [0])
+    assert dev.info()["layout"] == TEXPLICIT and dev.info()["bin_bits"] == 8
+    X = _inputs(trees, 200_000, 100, seed=5, special_frac=0.01)
+    want = port.lgb_predict_raw(trees, 1, 100, X)[:, 0]
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), want)
+    X32 = X[:50_000].astype(np.float32)
+    assert np.array_equal(dev.predict(X32, OUT_MARGIN),
+                          port.lgb_predict_raw(trees, 1, 100, X32.astype(np.float64))[:, 0])
