@@ -97,7 +97,10 @@ def test_c5_concurrent_http_serving():
         assert r["completed"] > 10000 and r["lost"] == 0
         assert r["non200"] == 0 and r["conn_errors"] == 0
         assert r["p50_ms"] >= 5.0 * 0.5          # requests do wait for their batch window
-        assert r["p99_ms"] < 100.0, r
+        # a request waits at most one window (5 ms) plus its batch's predict and
+        # the HTTP/JSON round trip: p99 within two windows (measured 6.6 ms on
+        # one MI355X, profiles/r3f_c5_serving.txt)
+        assert r["p99_ms"] <= 2 * 5.0, r
     finally:
         try:
             os.killpg(server.pid, signal.SIGTERM)
