@@ -166,6 +166,10 @@ typedef struct ti_forest_info {
   int32_t walk;               /* binned heap walk of float32 input: 0 indexed step
                                  (5 VALU), 1 fixed-layout step (4 VALU)  */
   int32_t bin_bits;           /* 8 or 16: bin width of the float32 image (0: none)   */
+  int32_t tree_ilp;           /* record layouts: trees walked at once per lane       */
+  int32_t n_stages;           /* staged layouts (7, 9): LDS stages of the forest     */
+  int32_t top_depth;          /* layouts 8, 9: levels of each tree's heap top        */
+  int32_t bottom;             /* layout 9: 0 records, 1 compact u8 nodes (plan_tx8)  */
 } ti_forest_info;
 
 /* Upload the forest to each listed device (HIP device ordinals).  HIP is

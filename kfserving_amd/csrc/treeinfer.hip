@@ -415,7 +415,10 @@ struct DeviceForest {
   uint2* rx_recs[2] = {nullptr, nullptr};
   uint32_t* rx_base = nullptr;
   uint32_t* rx_nint = nullptr;
-  int32_t* lx_stage = nullptr;   // staged record layout (7): first tree of each stage
+  int32_t* lx_stage = nullptr;
+  uint32_t* tx8_pos = nullptr;   // layout 9 compact bottom: first position of each tree
+  void* tx8_val = nullptr;       //   leaf value per bottom position (ACC)
+  int32_t* tx8_ord = nullptr;    //   leaf ordinal per bottom position   // staged record layout (7): first tree of each stage
   uint32_t* hx_top[2] = {nullptr, nullptr};   // heap tops of layout 8, per input dtype
   // TreeSHAP path tables
   ShapPath* shap_paths = nullptr;
@@ -499,6 +502,12 @@ struct ti_forest {
   // rx[i].top, tree byte offsets [T+1] and bottom internal counts [T]; stages
   // and ILP in h_lx_stage / lx_stage_cap / lx_ilp
   std::vector<uint32_t> h_tx_off, h_tx_nint;
+  // layout 9's compact u8 bottom (plan_tx8): per tree the first bottom
+  // position [T+1], and per bottom position the leaf value (ACC) / ordinal
+  int32_t tx8 = 0;
+  std::vector<uint32_t> h_tx8_pos;
+  std::vector<unsigned char> h_tx8_val;
+  std::vector<int32_t> h_tx8_ord;
   std::vector<int64_t> h_exp_src;   // explicit internal node -> descriptor node
   // TreeSHAP (TI_OUTPUT_CONTRIB); has_shap = 0 when the forest has no covers.
   // The path tables are built and uploaded on the first contributions call
@@ -554,6 +563,7 @@ void free_device(DeviceForest& d) {
                   d.bx_tbl[0], d.bx_tbl[1],
                   d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias,
                   d.rx_recs[0], d.rx_recs[1], d.rx_base, d.rx_nint, d.lx_stage,
+                  d.tx8_pos, d.tx8_val, d.tx8_ord,
                   d.hx_top[0], d.hx_top[1]};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -583,6 +593,9 @@ void free_device(DeviceForest& d) {
   d.rx_recs[0] = d.rx_recs[1] = nullptr;
   d.rx_base = d.rx_nint = nullptr;
   d.lx_stage = nullptr;
+  d.tx8_pos = nullptr;
+  d.tx8_val = nullptr;
+  d.tx8_ord = nullptr;
   d.hx_top[0] = d.hx_top[1] = nullptr;
   d.shap_paths = nullptr;
   d.shap_elems = nullptr;
@@ -1327,6 +1340,173 @@ bool plan_tx(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>&
   return true;
 }
 
+// Layout 9 with a compact bottom (u8 bins only; treeinfer_kernels.h,
+// t8explicit_predict_kernel).  A bottom node is one u32 -- the u8 record x
+// word (bin offset | flags | rank << 16) with byte 3 holding a pair index
+// k' -- and a node's children sit side by side at positions 2k', 2k' + 1, so
+// a step reads the bin and the children's 8-byte pair at once (one LDS round
+// trip, the bytes of layout 9's one record read) and selects the child.
+// Positions: the entries (nodes at depth D0 and leaves above it, in the
+// order the top reaches them) first, padded to an even count, then the
+// children of the bottom's internal nodes in breadth-first order (internal
+// node k's at n_entries + 2k), so k' = n_entries / 2 + k < 256 for trees of
+// <= 255 leaves.  A leaf loops on itself: x = kLeaf | rank 0xFF (even
+// position: never right, NaN-left) or rank 0 (odd: always right), bin offset
+// 0, k' = p / 2; its value and ordinal are read by position from global
+// tables when the group is walked.  Returns false (u8 layout 9 keeps its
+// records) when a tree has more than 255 leaves or the images do not fit.
+bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>& slot_of, int D) {
+  if (env_int("TI_TX8", 1) == 0 || !f->rx[0].b8 || !f->rx[1].b8) return false;
+  int D0 = env_int("TI_TX_TOP", 6);
+  D0 = std::max(1, std::min(D0, std::min(D, 10)));
+  const int T = d->n_trees;
+  const size_t NE = size_t(1) << D0;
+  const uint32_t topb = static_cast<uint32_t>(8 * NE);
+  const size_t acc_sz = f->accum == TI_F64 ? 8 : 4;
+  // per tree: entries (the top's cut, left to right), then BFS children
+  std::vector<std::vector<int32_t>> order(T);   // node at each bottom position (-1: pad)
+  std::vector<std::vector<uint32_t>> kpair(T);  // per node: its children's pair index (internal)
+  std::vector<uint32_t> pos(T + 1, 0), off(T + 1, 0);
+  std::vector<int32_t> dep;
+  struct Item { int32_t v; int l; };
+  std::vector<Item> st;
+  for (int t = 0; t < T; ++t) {
+    const int64_t b = d->tree_offset[t];
+    const int32_t n = static_cast<int32_t>(d->tree_offset[t + 1] - b);
+    if (static_cast<int64_t>(n) > 509) return false;   // > 255 leaves
+    std::vector<int32_t>& ord = order[t];
+    ord.clear();
+    // the top's cut in left-to-right order: depth-D0 nodes and shallow leaves
+    st.assign(1, Item{0, 0});
+    while (!st.empty()) {
+      const Item it = st.back();
+      st.pop_back();
+      const int64_t g = b + it.v;
+      if (it.l == D0 || d->feature[g] < 0) {
+        ord.push_back(it.v);
+        continue;
+      }
+      st.push_back(Item{d->right[g], it.l + 1});
+      st.push_back(Item{d->left[g], it.l + 1});
+    }
+    const size_t n_entries = ord.size();
+    if (n_entries & 1) ord.push_back(-1);
+    const uint32_t half = static_cast<uint32_t>(ord.size() / 2);
+    kpair[t].assign(n, 0u);
+    uint32_t k = 0;
+    for (size_t i = 0; i < ord.size(); ++i) {   // breadth-first over the bottom
+      const int32_t v = ord[i];
+      if (v < 0 || d->feature[b + v] < 0) continue;
+      if (half + k > 255) return false;
+      kpair[t][v] = half + k++;
+      ord.push_back(d->left[b + v]);
+      ord.push_back(d->right[b + v]);
+    }
+    pos[t + 1] = pos[t] + static_cast<uint32_t>(ord.size());
+    const uint64_t bytes = topb + ((static_cast<uint64_t>(ord.size()) * 4 + 15) & ~uint64_t(15));
+    if (bytes > 65520 || off[t] + bytes > 0xFFFFFFF0ull) return false;
+    off[t + 1] = off[t] + static_cast<uint32_t>(bytes);
+  }
+  // stages: as plan_tx
+  const int R = f->rx[0].rows;
+  if (f->rx[1].rows != R) return false;
+  const size_t bins = align16(static_cast<size_t>(std::max(f->rx[0].words, f->rx[1].words)) * R * 4 + 4);
+  const int wgs = std::max(1, env_int("TI_LX_WGS", 2));
+  size_t cap = kLdsPerCu / static_cast<size_t>(wgs);
+  cap = cap > bins ? cap - bins : 0;
+  cap = std::min(cap, static_cast<size_t>(kLxPf) * 16 * R) & ~size_t(15);
+  size_t biggest = 0;
+  for (int t = 0; t < T; ++t) biggest = std::max<size_t>(biggest, off[t + 1] - off[t]);
+  if (T < 2 || cap < 2 * biggest) return false;
+  // trees walked at once per lane: 4 (TI_LX_ILP overrides).  A stage holds a
+  // whole number of ILP groups where it can (a group wider than the rest of
+  // its stage walks duplicate trees): on c3_maxbin at 12 trees a stage, ILP 4
+  // 4.70 ms, 7 5.29, 8 5.72 (profiles/r3_tx8_sweep.jsonl)
+  const int force_ilp = env_int("TI_LX_ILP", 0);
+  const int ilp = force_ilp > 0 ? (force_ilp >= 8 ? 8 : force_ilp == 7 ? 7 : 4) : 4;
+  std::vector<int32_t> stages(1, 0);
+  int t0 = 0;
+  while (t0 < T) {
+    int t1 = t0 + 1;
+    while (t1 < T && off[t1 + 1] - off[t0] <= cap) ++t1;
+    if (t1 < T && t1 - t0 > ilp) t1 = t0 + ((t1 - t0) / ilp) * ilp;
+    stages.push_back(t1);
+    t0 = t1;
+  }
+  // position tables (shared by the views): leaf value and ordinal
+  f->h_tx8_val.assign(static_cast<size_t>(pos[T]) * acc_sz, 0);
+  f->h_tx8_ord.assign(pos[T], 0);
+  for (int t = 0; t < T; ++t) {
+    const int64_t b = d->tree_offset[t];
+    for (uint32_t p = 0; p < pos[t + 1] - pos[t]; ++p) {
+      const int32_t v = order[t][p];
+      if (v < 0 || d->feature[b + v] >= 0) continue;
+      const size_t at = pos[t] + p;
+      f->h_tx8_ord[at] = static_cast<int32_t>(slot_of[b + v] - f->h_rx_nint[t]);
+      if (acc_sz == 8) {
+        const double x = d->leaf_value[(b + v) * d->leaf_width];
+        std::memcpy(&f->h_tx8_val[at * 8], &x, 8);
+      } else {
+        const float x = static_cast<float>(d->leaf_value[(b + v) * d->leaf_width]);
+        std::memcpy(&f->h_tx8_val[at * 4], &x, 4);
+      }
+    }
+  }
+  // images per view
+  constexpr uint32_t kLeaf = ti::RxBins<true>::kLeaf, kNanLeft = ti::RxBins<true>::kNanLeft;
+  std::vector<int32_t> entry_of;
+  for (auto& rx : f->rx) {
+    rx.top.assign(off[T] / 4, 0u);
+    for (int t = 0; t < T; ++t) {
+      const int64_t b = d->tree_offset[t];
+      const int32_t n = static_cast<int32_t>(d->tree_offset[t + 1] - b);
+      uint32_t* top = &rx.top[off[t] / 4];
+      uint32_t* bot = top + 2 * NE;
+      const std::vector<int32_t>& ord = order[t];
+      entry_of.assign(n, -1);
+      for (uint32_t p = 0; p < ord.size(); ++p) {
+        const int32_t v = ord[p];
+        if (v < 0) {
+          bot[p] = kLeaf | (p & 1 ? 0u : (0xFF0000u | kNanLeft)) | ((p >> 1) << 24);
+          continue;
+        }
+        if (entry_of[v] < 0) entry_of[v] = static_cast<int32_t>(p);
+        const int64_t g = b + v;
+        if (d->feature[g] < 0)
+          bot[p] = kLeaf | (p & 1 ? 0u : (0xFF0000u | kNanLeft)) | ((p >> 1) << 24);
+        else
+          bot[p] = rx.recs[b + slot_of[g]].x | (kpair[t][v] << 24);
+      }
+      // the top: x words, and at depth D0 the entry position
+      struct TItem { int32_t v; uint32_t hp; int l; };
+      std::vector<TItem> ts(1, TItem{0, 1u, 0});
+      while (!ts.empty()) {
+        const TItem it = ts.back();
+        ts.pop_back();
+        const int64_t g = b + it.v;
+        if (it.l == D0) {
+          top[it.hp] = static_cast<uint32_t>(entry_of[it.v]);
+          continue;
+        }
+        const bool leaf = d->feature[g] < 0;
+        top[it.hp] = leaf ? kHxPad8 : rx.recs[b + slot_of[g]].x;
+        ts.push_back(TItem{leaf ? it.v : d->left[g], 2 * it.hp, it.l + 1});
+        ts.push_back(TItem{leaf ? it.v : d->right[g], 2 * it.hp + 1, it.l + 1});
+      }
+    }
+  }
+  f->h_tx_off = off;
+  f->h_tx8_pos = pos;
+  f->h_tx_nint.assign(T, 0);
+  f->h_lx_stage = stages;
+  f->lx_stage_cap = static_cast<int64_t>(cap);
+  f->lx_ilp = ilp;
+  f->hx_top = D0;
+  f->tx8 = 1;
+  f->layout = 9;
+  return true;
+}
+
 // Mean depth of the leaves of a forest (every leaf counted once).
 double mean_leaf_depth(const ti_forest_desc* d) {
   double sum = 0;
@@ -1512,6 +1692,13 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
     }
     if ((rc = upload(&d.rx_base, f->h_tx_off, &d.bytes))) return rc;
     if ((rc = upload(&d.rx_nint, f->h_tx_nint, &d.bytes))) return rc;
+    if (f->tx8) {
+      if ((rc = upload(&d.tx8_pos, f->h_tx8_pos, &d.bytes))) return rc;
+      unsigned char* tv = nullptr;
+      if ((rc = upload(&tv, f->h_tx8_val, &d.bytes))) return rc;
+      d.tx8_val = tv;
+      if ((rc = upload(&d.tx8_ord, f->h_tx8_ord, &d.bytes))) return rc;
+    }
     if ((rc = upload(&d.lx_stage, f->h_lx_stage, &d.bytes))) return rc;
     if ((rc = upload(&d.leaf_base, f->h_leaf_base, &d.bytes))) return rc;
     if (f->LW > 1) {   // vector leaves are read from the leaf table
@@ -1592,6 +1779,13 @@ KernelFn select_texplicit(int xdt, int accum, int K, bool z, int ilp, bool b8) {
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(9, K, true, z, !b8, ilp);
   if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(9, K, true, z, !b8, ilp);
   return ti::kernels_df(9, K, true, z, !b8, ilp);
+}
+
+KernelFn select_t8explicit(int xdt, int accum, int K, bool z, int ilp) {   // layout 9, compact u8 bottom
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(11, K, true, z, false, ilp);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(11, K, true, z, false, ilp);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(11, K, true, z, false, ilp);
+  return ti::kernels_df(11, K, true, z, false, ilp);
 }
 
 KernelFn select_hexplicit(int xdt, int accum, int K, bool z, int ilp) {
@@ -1859,7 +2053,11 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (lds > kLdsPerCu || static_cast<int64_t>(kLxPf) * 16 * R < f->lx_stage_cap)
       return fail(TI_ERR_UNSUPPORTED, "heap-top staged layout exceeds LDS");
     a.bin_chunk = bin_chunk_for(static_cast<size_t>(f->lx_stage_cap), R, xdt, f->F);
-    KernelFn fn = select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp, rx.b8 != 0);
+    a.tx_pos = d.tx8_pos;
+    a.tx_vals = d.tx8_val;
+    a.tx_ord = d.tx8_ord;
+    KernelFn fn = f->tx8 ? select_t8explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
+                         : select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp, rx.b8 != 0);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
@@ -2598,7 +2796,8 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
       const bool try8 = rx_ok && env_int("TI_RX_B8", 1) != 0 &&
                         (want.empty() || want == "texplicit") &&
                         env_int("TI_NO_TEXPLICIT", 0) == 0;
-      bool b8 = try8 && pack_views(true) && plan_tx(desc, f.get(), slot_of, D);
+      bool b8 = try8 && pack_views(true) &&
+                (plan_tx8(desc, f.get(), slot_of, D) || plan_tx(desc, f.get(), slot_of, D));
       if (!b8 && rx_ok) rx_ok = pack_views(false);
       if (rx_ok) {
         f->layout = 6;
@@ -2660,6 +2859,8 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
     rx.tbl.clear();
     rx.tbl.shrink_to_fit();
   }
+  f->h_tx8_val.clear(); f->h_tx8_val.shrink_to_fit();
+  f->h_tx8_ord.clear(); f->h_tx8_ord.shrink_to_fit();
   f->h_rx_base.clear(); f->h_rx_base.shrink_to_fit();
   f->h_rx_nint.clear(); f->h_rx_nint.shrink_to_fit();
   for (auto& bi : f->bh) {
@@ -2700,6 +2901,12 @@ int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
   info->walk = bheap_fixed(f, TI_F32, TI_OUTPUT_PREDICT) ? 1 : 0;
   info->bin_bits = f->layout == 3 ? (f->bh[0].b16 ? 16 : 8)
                    : (f->layout >= 6 && f->layout <= 9) ? (f->rx[0].b8 ? 8 : 16) : 0;
+  info->tree_ilp = f->layout == 6 ? f->rx_ilp : f->layout == 8 ? f->hx_ilp
+                   : (f->layout == 7 || f->layout == 9) ? f->lx_ilp : 0;
+  info->n_stages = (f->layout == 7 || f->layout == 9) && !f->h_lx_stage.empty()
+                       ? static_cast<int32_t>(f->h_lx_stage.size() - 1) : 0;
+  info->top_depth = (f->layout == 8 || f->layout == 9) ? f->hx_top : 0;
+  info->bottom = f->layout == 9 ? f->tx8 : 0;
   return TI_OK;
 }
 

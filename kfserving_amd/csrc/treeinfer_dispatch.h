@@ -12,7 +12,7 @@ using KernelFn = void (*)(KArgs);
 // layout: 0 heap, 1 explicit, 3 binned heap, 6 record explicit, 7 staged
 // record explicit, 8 heap top + record bottom, 9 heap top + staged record
 // bottom (2, 4 and 5 were retired in round 3); 10 selects the fixed-layout
-// walk of layout 3 (bheap_fix_kernel).
+// walk of layout 3 (bheap_fix_kernel), 11 layout 9's compact u8 bottom.
 // fl: feature image in
 // LDS; z: LightGBM zero rule; b16 / pf: binned heap (and layout 9) bin width
 // and prefetch depth.
@@ -30,6 +30,16 @@ KernelFn select_tx(bool z, int pf) {
 
 template <typename XT, typename ACC, int KMAX>
 KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
+  if (layout == 11) {   // layout 9 with the compact u8 bottom; pf carries the tree ILP
+    if constexpr (sizeof(ACC) == 8) {
+      if (z) return pf >= 8 ? t8explicit_predict_kernel<XT, ACC, KMAX, true, 8>
+                    : pf == 7 ? t8explicit_predict_kernel<XT, ACC, KMAX, true, 7>
+                              : t8explicit_predict_kernel<XT, ACC, KMAX, true, 4>;
+    }
+    return pf >= 8 ? t8explicit_predict_kernel<XT, ACC, KMAX, false, 8>
+           : pf == 7 ? t8explicit_predict_kernel<XT, ACC, KMAX, false, 7>
+                     : t8explicit_predict_kernel<XT, ACC, KMAX, false, 4>;
+  }
   if (layout == 9) {   // pf carries the tree ILP (4, 7 or 8); b16 false: u8 bins
     if (!b16) return select_tx<XT, ACC, KMAX, true>(z, pf);
     return select_tx<XT, ACC, KMAX, false>(z, pf);

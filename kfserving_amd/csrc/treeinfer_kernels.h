@@ -105,6 +105,10 @@ struct KArgs {
   // staged record layouts (7, 9)
   const int32_t* stage_start;     // [n_stages+1] first tree of each LDS stage
   int32_t n_stages;
+  // layout 9's compact u8 bottom (t8explicit_predict_kernel)
+  const uint32_t* tx_pos;         // [T+1] first bottom position of each tree
+  const void* tx_vals;            // [positions] leaf value (ACC)
+  const int32_t* tx_ord;          // [positions] leaf ordinal in its tree
   // binned layouts: rank images of the features (see stage_bins)
   const void* bin_tbl;            // [F][2^bin_L] Eytzinger threshold tables, XT
   int32_t bin_L;                  // search depth (common to all features)
@@ -1103,11 +1107,16 @@ constexpr uint32_t kRxOffMask = 0xFFFAu;   // the bin byte offset without the fl
 // tile holding a NaN takes the slow step, which tests b == 0 first.
 template <bool B8> struct RxBins {
   static constexpr uint32_t kNanLeft = 1u, kZeroFlip = 4u, kOffMask = 0xFFFAu;
+  static constexpr uint32_t kLeaf = 0u;   // (the compact bottom is u8 only)
   template <bool ZERO> static constexpr uint32_t nan_code() { return ZERO ? 0xFFFEu : 0xFFFFu; }
   static constexpr int kPerWord = 2;
 };
 template <> struct RxBins<true> {
   static constexpr uint32_t kNanLeft = 4u, kZeroFlip = 8u, kOffMask = 0xFFF3u;
+  // the compact bottom (t8explicit): a leaf's x carries kLeaf (bit 4, in the
+  // lane part); kNodeMask clears the flags, the leaf bit, the rank (byte 2)
+  // and the pair index (byte 3) from a bin address
+  static constexpr uint32_t kLeaf = 16u, kNodeMask = 0xFFE3u;
   template <bool ZERO> static constexpr uint32_t nan_code() { return 0u; }
   static constexpr int kPerWord = 4;
 };
@@ -1886,6 +1895,191 @@ __global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
       else tx_stage<ACC, KMAX, ZERO, false, false, ILP, B8>(a, acc, t0, t1, sbase, lane_off, row, live);
     }
   }
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
+
+// ---- layout 9 with the compact u8 bottom (plan_tx8) ------------------------
+// Top as layout 9's (the rank is byte 2 of an x word here, so the compare
+// selects BYTE_2; byte 3 holds the pair index); then per bottom step one LDS
+// round trip: the u8 bin of the lane's node and the 8-byte pair of its
+// children (position 2k', k' = byte 3) at once, one compare and one select,
+// no lane mask: a leaf's word loops on itself (rank 0xFF at even positions,
+// 0 at odd ones).  The group's loop ends when every lane of every tree holds
+// a leaf word (kLeaf in all of them).  A leaf's position 2k' + (rank == 0)
+// indexes the forest's position tables: the value (VIS) is loaded when the
+// group ends and added when the next group ends (tree order kept, the load's
+// latency hidden behind a walk); ordinals (leaf ids, vector leaves) at once.
+template <bool ZERO>
+__device__ __forceinline__ bool t8_right_slow(uint32_t x, uint32_t b) {
+  using W = RxBins<true>;
+  bool right = ((x >> 16) & 0xFFu) < b;
+  if (ZERO) right = right != (((b & 1u) != 0u) && ((x & W::kZeroFlip) != 0u));
+  if (b == 0u) right = (x & W::kNanLeft) == 0u;
+  return right;
+}
+
+template <typename ACC, int KMAX, int ILP>
+__device__ __forceinline__ void t8_flush(const KArgs& a, ACC (&acc)[KMAX], const ACC (&pend)[ILP],
+                                         const int (&pend_t)[ILP]) {
+#pragma unroll
+  for (int q = 0; q < ILP; ++q)
+    if (pend_t[q] >= 0) add_leaf<ACC, KMAX>(acc, &pend[q], 0, 1, a.tree_group[pend_t[q]]);
+}
+
+template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP>
+__device__ __forceinline__ void t8_stage(const KArgs& a, ACC (&acc)[KMAX], int t0, int t1,
+                                         uint32_t sbase, uint32_t lane_off, int64_t row, bool live,
+                                         ACC (&pend)[ILP], int (&pend_t)[ILP]) {
+  using W = RxBins<true>;
+  rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* tx_pos = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.tx_pos));
+  const int D0 = a.depth;
+  const uint32_t topb = 8u << D0;   // 2^(D0+1) u32
+  for (int j = t0; j < t1; j += ILP) {
+    uint32_t base[ILP], idx[ILP], nd[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = (j + q) < t1 ? (j + q) : (t1 - 1);
+      base[q] = sbase + tx_off[tq];
+      idx[q] = 1u;
+      nd[q] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+          static_cast<uintptr_t>(base[q] + 4u));   // the root: one broadcast read
+    }
+    for (int l = 0; l < D0; ++l) {   // the last level selects the bottom entry
+      uint32_t b[ILP];
+      rx_u2_t pr[ILP];
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        b[q] = lds_u8((nd[q] & W::kNodeMask) | lane_off);
+        pr[q] = lx_rec(base[q] + 8u * idx[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        if (!SLOW) {
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %2 src0_sel:BYTE_2 src1_sel:DWORD\n\t"
+              "v_cndmask_b32 %0, %3, %4, vcc\n\t"
+              "v_addc_co_u32 %1, vcc, %1, %1, vcc"
+              : "+v"(nd[q]), "+v"(idx[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y)
+              : "vcc");
+        } else {
+          const bool right = t8_right_slow<ZERO>(nd[q], b[q]);
+          idx[q] = idx[q] + idx[q] + (uint32_t)right;
+          nd[q] = right ? pr[q].y : pr[q].x;
+        }
+      }
+    }
+    uint32_t x[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      base[q] += topb;   // the bottom: u32 words by position
+      x[q] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+          static_cast<uintptr_t>(base[q] + 4u * nd[q]));
+    }
+    for (;;) {
+      uint32_t all = x[0];
+#pragma unroll
+      for (int q = 1; q < ILP; ++q) all &= x[q];
+      if (__ballot((all & W::kLeaf) == 0u) == 0) break;   // every lane of every tree at a leaf
+      uint32_t b[ILP];
+      rx_u2_t pr[ILP];
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        b[q] = lds_u8((x[q] & W::kNodeMask) | lane_off);
+        pr[q] = lx_rec(base[q] + ((x[q] >> 24) << 3));
+      }
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        if (!SLOW) {
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %1 src0_sel:BYTE_2 src1_sel:DWORD\n\t"
+              "v_cndmask_b32 %0, %2, %3, vcc"
+              : "+v"(x[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y) : "vcc");
+        } else {
+          x[q] = t8_right_slow<ZERO>(x[q], b[q]) ? pr[q].y : pr[q].x;
+        }
+      }
+    }
+    uint32_t li[ILP];   // the leaf's index in the position tables
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = (j + q) < t1 ? (j + q) : (t1 - 1);
+      li[q] = tx_pos[tq] + ((x[q] >> 23) & ~1u) + (((x[q] >> 16) & 0xFFu) == 0u ? 1u : 0u);
+    }
+    if (VIS) {
+      t8_flush<ACC, KMAX, ILP>(a, acc, pend, pend_t);   // the previous group's leaves
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        pend[q] = static_cast<const ACC*>(a.tx_vals)[li[q]];
+        pend_t[q] = (j + q) < t1 ? (j + q) : -1;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        const int t = j + q;
+        if (t < t1) {
+          const int64_t lf = a.leaf_base[t] + (int64_t)a.tx_ord[li[q]];
+          if (a.kind == TI_OUTPUT_LEAF) {
+            if (live) static_cast<int32_t*>(a.out)[row * a.n_trees + t] = a.exp_leaf_ids[lf];
+          } else {
+            add_leaf<ACC, KMAX>(acc, static_cast<const ACC*>(a.leaves) + lf * a.leaf_width, 0,
+                                a.leaf_width, a.tree_group[t]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
+__global__ void __launch_bounds__(512) t8explicit_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int PF = 8;   // = kLxPf (host): a stage is at most PF x 16 B x R
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  u32x4* stage = reinterpret_cast<u32x4*>(smem + a.stage_off);
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* sst = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.stage_start));
+  const unsigned char* img = a.trees;
+  const int NS = a.n_stages;
+  auto lo_of = [&](int s) { return tx_off[sst[s]]; };   // trees start 16-byte aligned
+  auto n16_of = [&](int s) { return (int)((tx_off[sst[s + 1]] - tx_off[sst[s]]) >> 4); };
+  u32x4 pf[PF];
+  prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(0)), n16_of(0), tid, R);
+  const bool slow = rx_stage_bins<XT, ZERO, false, true>(flag, a, row0, R, tid, stage);
+  const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
+  ACC acc[KMAX];
+  init_acc(acc, a);
+  ACC pend[ILP];   // the previous group's leaf values (t8_stage)
+  int pend_t[ILP];
+#pragma unroll
+  for (int q = 0; q < ILP; ++q) {
+    pend[q] = ACC(0);
+    pend_t[q] = -1;
+  }
+  for (int s = 0; s < NS; ++s) {
+    const int t0 = (int)sst[s], t1 = (int)sst[s + 1];
+    const uint32_t lo = lo_of(s);
+    __syncthreads();   // the previous stage's walk is over
+    commit_u<PF>(pf, stage, n16_of(s), tid, R);
+    __syncthreads();
+    const int sn = s + 1 < NS ? s + 1 : s;
+    prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(sn)), n16_of(sn), tid, R);
+    const uint32_t sbase = (uint32_t)a.stage_off - lo;   // LDS address = sbase + image byte
+    if (slow) {
+      if (vis) t8_stage<ACC, KMAX, ZERO, true, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
+      else t8_stage<ACC, KMAX, ZERO, true, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
+    } else {
+      if (vis) t8_stage<ACC, KMAX, ZERO, false, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
+      else t8_stage<ACC, KMAX, ZERO, false, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
+    }
+  }
+  if (vis) t8_flush<ACC, KMAX, ILP>(a, acc, pend, pend_t);
   if (!live || a.kind == TI_OUTPUT_LEAF) return;
   finish_row<ACC, KMAX>(acc, a, row);
 }

@@ -85,6 +85,10 @@ class _ForestInfo(ctypes.Structure):
         ("tree_stride_bytes", ctypes.c_int64),
         ("walk", ctypes.c_int32),
         ("bin_bits", ctypes.c_int32),
+        ("tree_ilp", ctypes.c_int32),
+        ("n_stages", ctypes.c_int32),
+        ("top_depth", ctypes.c_int32),
+        ("bottom", ctypes.c_int32),
     ]
 
 

@@ -67,7 +67,9 @@ def main():
     info = dev.info()
     print(json.dumps({"workload": a.workload, "rows": a.rows, "dtype": dtype,
                       "layout": bench.LAYOUT_NAMES.get(info["layout"]), "walk": info["walk"],
-                      "bin_bits": info["bin_bits"], "kernel_ms": ms,
+                      "bin_bits": info["bin_bits"], "tree_ilp": info["tree_ilp"],
+                      "n_stages": info["n_stages"], "top_depth": info["top_depth"],
+                      "bottom": info["bottom"], "kernel_ms": ms,
                       "rows_per_s": a.rows / (ms * 1e-3)}), flush=True)
     dev.close()
 

@@ -48,6 +48,42 @@ def _inputs(trees, rows, F, seed, special_frac=0.03, at_frac=0.05):
     return X
 
 
+def _lone_leaf(value=0.25):
+    z = np.zeros(0, dtype=np.int64)
+    return {"split_feature": z, "threshold": np.zeros(0), "decision_type": z, "left_child": z,
+            "right_child": z, "leaf_value": np.array([value]), "leaf_count": np.array([10]),
+            "internal_count": z}
+
+
+@pytest.mark.parametrize("top", [1, 3, 6, 9])
+@pytest.mark.parametrize("tx8", [1, 0])
+def test_u8_bottoms_every_top_depth(monkeypatch, top, tx8):
+    """Layout 9's two u8 bottoms (TI_TX8=1: compact u32 nodes with their
+    children side by side, leaves looping on themselves; 0: layout 7's
+    records) at top depths that end above, inside and below the trees, with a
+    one-split tree and a lone leaf among them, NaN / zero / 1e-36 rows in some
+    tiles: margins and leaf ids bit-exact against the C port."""
+    monkeypatch.setenv("TI_TX_TOP", str(top))
+    monkeypatch.setenv("TI_TX8", str(tx8))
+    mts = (MISSING_NONE, MISSING_ZERO, MISSING_NAN)
+    trees = lf.synthetic_maxbin_trees(29, 255, 30, seed=top, max_bin=125, missing_types=mts)
+    trees.insert(5, lf.synthetic_maxbin_trees(1, 2, 30, seed=99, max_bin=125)[0])
+    trees.insert(11, _lone_leaf())
+    f = _forest(trees, 30)
+    dev = DeviceForest(f, [0])
+    assert dev.info()["layout"] == TEXPLICIT and dev.info()["bin_bits"] == 8
+    X = _inputs(trees, 3001, 30, seed=top + 7, special_frac=0.02)
+    X[:1024][~np.isfinite(X[:1024])] = 0.5           # fast tiles first
+    X[:1024][X[:1024] == 0] = 0.5
+    for Xi in (X, X.astype(np.float32)):
+        want = port.lgb_predict_raw(trees, 1, 30, Xi.astype(np.float64))[:, 0]
+        assert np.array_equal(dev.predict(Xi, OUT_MARGIN), want)
+    monkeypatch.setenv("TI_FORCE_LAYOUT", "rexplicit")
+    ref = DeviceForest(f, [0])
+    X32 = X.astype(np.float32)
+    assert np.array_equal(dev.predict(X32, OUT_LEAF), ref.predict(X32, OUT_LEAF))
+
+
 @pytest.mark.parametrize("missing", ["none", "all"])
 def test_maxbin_u8_matches_port_and_u16(monkeypatch, missing):
     mts = (MISSING_NONE,) if missing == "none" else (MISSING_NONE, MISSING_ZERO, MISSING_NAN)
