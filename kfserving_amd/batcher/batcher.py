@@ -61,6 +61,12 @@ class Batcher:
     async def submit(self, instances: List[Any]) -> Dict[str, Any]:
         """Queue one request's rows: a list, or a 2-D matrix decoded natively
         from the body (kfserving.fastjson.JsonInstances)."""
+        return await self.enqueue(instances)
+
+    def enqueue(self, instances: List[Any]) -> "asyncio.Future":
+        """submit() without the coroutine: queue the rows and return the future
+        their response resolves (for callers that attach a callback instead of
+        awaiting, such as bench.py's open-loop load)."""
         if isinstance(instances, np.ndarray):
             if instances.ndim != 2 or instances.shape[0] == 0:
                 raise HTTPError(400, "no instances in the request")
@@ -79,7 +85,7 @@ class Batcher:
         elif self._timer is None:
             delay = self.max_latency_ms / 1000.0 - (time.monotonic() - self._start)
             self._timer = loop.call_later(max(delay, 0.0), self._flush)
-        return await fut
+        return fut
 
     def _flush(self) -> None:
         if self._timer is not None:
