@@ -350,7 +350,8 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
 
     import gc
     old = gc.get_threshold()
-    if freeze_gc:          # what KFServer.start does after load (kfserver.tune_gc)
+    old_si = sys.getswitchinterval()
+    if freeze_gc:          # what KFServer.start does after load (kfserver.tune_gc: GC, GIL interval)
         from kfserving_amd.kfserving.kfserver import tune_gc
         tune_gc()
     try:
@@ -359,6 +360,7 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
         if freeze_gc:
             gc.unfreeze()
             gc.set_threshold(*old)
+            sys.setswitchinterval(old_si)
     pool_ex.shutdown()
     lat_ms = lat[warm:] * 1e3
     return {"qps_offered": qps, "requests": n_req - warm, "rows_per_request": "U{1..64}",

@@ -86,10 +86,16 @@ def tune_gc() -> None:
     """Move the loaded models / parsed forests to the permanent generation and
     make young-generation collections rarer: with thousands of in-flight
     request futures, default gen-2 pauses reached 300 ms at p99 (measured in
-    bench.py's batched-latency leg at 10k requests/s; 8 ms with this)."""
+    bench.py's batched-latency leg at 10k requests/s; 8 ms with this).
+
+    Also shorten the interpreter's GIL switch interval (5 ms by default) to
+    0.5 ms: a predict thread returning from ti_predict (which drops the GIL)
+    waits for the event loop's thread to hand the GIL back, up to one switch
+    interval, and that wait sat in the tail of every batch's latency."""
     gc.collect()
     gc.freeze()
     gc.set_threshold(50_000, 50, 100)
+    sys.setswitchinterval(min(sys.getswitchinterval(), 0.0005))
 
 
 def gpu_count_without_init() -> int:
