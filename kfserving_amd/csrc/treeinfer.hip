@@ -890,18 +890,21 @@ void eytzinger_tables(const RankTables<XT>& rt, std::vector<unsigned char>* out)
 // +inf padding.  The search counts the keys below x at each node and descends;
 // after H levels, j - (5^H - 1)/4 = #{u < x}: the same rank as the Eytzinger
 // search, in H 16-byte gathers instead of L 4-byte ones.
-void kary_fill(const std::vector<float>& srt, std::vector<float>* out, size_t j, int level, int H,
+template <typename XT>
+void kary_fill(const std::vector<XT>& srt, std::vector<XT>* out, size_t j, int level, int H,
                size_t* i) {
   if (level == H) return;
   for (int c = 0; c < 4; ++c) {
     kary_fill(srt, out, 5 * j + 1 + c, level + 1, H, i);
-    (*out)[4 * j + c] = *i < srt.size() ? srt[*i] : INFINITY;
+    (*out)[4 * j + c] = *i < srt.size() ? srt[*i] : static_cast<XT>(INFINITY);
     ++*i;
   }
   kary_fill(srt, out, 5 * j + 5, level + 1, H, i);
 }
 
-void kary_tables(const RankTables<float>& rt, std::vector<unsigned char>* out, int* height) {
+// (float32 view: 16-byte nodes; float64 view: 32-byte nodes of 4 doubles)
+template <typename XT>
+void kary_tables(const RankTables<XT>& rt, std::vector<unsigned char>* out, int* height) {
   const int F = static_cast<int>(rt.u.size());
   int H = 1;
   size_t p5 = 5;
@@ -910,13 +913,14 @@ void kary_tables(const RankTables<float>& rt, std::vector<unsigned char>* out, i
     ++H;
   }
   const size_t nn = (p5 - 1) / 4;
-  out->assign(static_cast<size_t>(F) * nn * 16, 0);
-  std::vector<float> node(nn * 4), srt;
+  out->assign(static_cast<size_t>(F) * nn * 4 * sizeof(XT), 0);
+  std::vector<XT> node(nn * 4), srt;
   for (int f = 0; f < F; ++f) {
     srt.assign(rt.u[f].begin(), rt.u[f].end());
     size_t i = 0;
     kary_fill(srt, &node, 0, 0, H, &i);
-    std::memcpy(out->data() + static_cast<size_t>(f) * nn * 16, node.data(), nn * 16);
+    std::memcpy(out->data() + static_cast<size_t>(f) * nn * 4 * sizeof(XT), node.data(),
+                nn * 4 * sizeof(XT));
   }
   *height = H;
 }
@@ -1067,12 +1071,9 @@ bool pack_rexplicit(const ti_forest_desc* d, const ti_forest* f,
   rx->rows = R;
   rx->L = rt.L;
   rx->kary = 0;
-  if constexpr (sizeof(XT) == 4) {
-    if (env_int("TI_KARY", 1) != 0) kary_tables(rt, &rx->tbl, &rx->kary);
-    else eytzinger_tables(rt, &rx->tbl);
-  } else {
-    eytzinger_tables(rt, &rx->tbl);
-  }
+  // 5-ary tables for both views (float64: TI_KARY64, 32-byte nodes)
+  if (env_int(sizeof(XT) == 4 ? "TI_KARY" : "TI_KARY64", 1) != 0) kary_tables(rt, &rx->tbl, &rx->kary);
+  else eytzinger_tables(rt, &rx->tbl);
   // an even slot count: the staged layout copies whole 16-byte words
   rx->recs.assign(d->n_nodes + (d->n_nodes & 1), uint2{0u, 0u});
   const bool scalar_leaves = d->leaf_width == 1;

@@ -547,7 +547,7 @@ __device__ __forceinline__ void rank_search(const KArgs& a, const XT (&x)[Q], in
       for (int q = 0; q < Q; ++q) e[q] = t4[tq[q] + k[q]];
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        const float xv = (float)x[q];
+        const XT xv = x[q];
         const uint32_t c = (e[q].x < xv ? 1u : 0u) + (e[q].y < xv ? 1u : 0u) +
                            (e[q].z < xv ? 1u : 0u) + (e[q].w < xv ? 1u : 0u);
         k[q] = 5u * k[q] + 1u + c;
@@ -1203,10 +1203,10 @@ __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], i
   const uint32_t tsz = 1u << a.bin_L;
   uint32_t tq[Q], k[Q];
   if (KARY) {
-    // 5-ary search tree (float32 view): node j holds 4 sorted keys in 16 B,
-    // its children are 5j+1 .. 5j+5; after H levels j - (5^H - 1)/4 is the
-    // number of keys below x.  H gathers instead of L.
-    typedef float f4_t __attribute__((ext_vector_type(4)));
+    // 5-ary search tree: node j holds 4 sorted keys (16 B for the float32
+    // view, 32 B for float64), its children are 5j+1 .. 5j+5; after H levels
+    // j - (5^H - 1)/4 is the number of keys below x.  H gathers instead of L.
+    typedef XT f4_t __attribute__((ext_vector_type(4)));
     const f4_t* t4 = reinterpret_cast<const f4_t*>(a.bin_tbl);
     const uint32_t nn = (kpow5(a.bin_kary) - 1u) / 4u;   // nodes per feature
 #pragma unroll
@@ -1221,7 +1221,7 @@ __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], i
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const f4_t e = s4[tq[q]];
-        const float xv = (float)x[q];
+        const XT xv = x[q];
         k[q] = 1u + (e.x < xv ? 1u : 0u) + (e.y < xv ? 1u : 0u) + (e.z < xv ? 1u : 0u) +
                (e.w < xv ? 1u : 0u);
       }
@@ -1233,7 +1233,7 @@ __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], i
       for (int q = 0; q < Q; ++q) e[q] = t4[tq[q] + k[q]];
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        const float xv = (float)x[q];
+        const XT xv = x[q];
         const uint32_t c = (e[q].x < xv ? 1u : 0u) + (e[q].y < xv ? 1u : 0u) +
                            (e[q].z < xv ? 1u : 0u) + (e[q].w < xv ? 1u : 0u);
         k[q] = 5u * k[q] + 1u + c;
@@ -1347,18 +1347,16 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
   return *flag != 0;
 }
 
-// The float32 view searches the 5-ary tables when the host built them
-// (a.bin_kary > 0), every other view the Eytzinger tables.
+// Both views search the 5-ary tables when the host built them (a.bin_kary >
+// 0: float32 16-byte nodes, float64 32-byte ones), else the Eytzinger tables.
 // SROOT: the 5-ary root as a scalar load (layout 8: C4 2.17 -> 2.13 ms; on
 // layout 9 it cost C3 0.7 %, profiles/r2_kary_root_sweep.jsonl)
 template <typename XT, bool ZB, bool SROOT = false, bool B8 = false>
 __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
                                               int R, int tid, void* temp = nullptr) {
-  if constexpr (sizeof(XT) == 4) {
-    if (a.bin_kary > 0)
-      return rx_stage_bins_impl<XT, ZB, true, SROOT, B8>(flag, static_cast<XT*>(temp), a, row0, R,
-                                                         tid);
-  }
+  if (a.bin_kary > 0)
+    return rx_stage_bins_impl<XT, ZB, true, SROOT, B8>(flag, static_cast<XT*>(temp), a, row0, R,
+                                                       tid);
   return rx_stage_bins_impl<XT, ZB, false, false, B8>(flag, static_cast<XT*>(temp), a, row0, R, tid);
 }
 
