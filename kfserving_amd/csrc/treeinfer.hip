@@ -1286,11 +1286,16 @@ bool plan_tx(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>&
     f->h_tx_nint.clear();
     return false;
   }
+  // TI_LX_ILP > 0 also cuts stages to whole groups of that many trees
+  // (plan_tx8 always does; here the default ILP follows the stage size)
+  const int force_ilp = env_int("TI_LX_ILP", 0);
+  const int cut = force_ilp > 0 ? (force_ilp >= 8 ? 8 : force_ilp == 7 ? 7 : 4) : 0;
   std::vector<int32_t> stages(1, 0);
   int t0 = 0;
   while (t0 < T) {
     int t1 = t0 + 1;
     while (t1 < T && o[t1 + 1] - o[t0] <= cap) ++t1;
+    if (cut && t1 < T && t1 - t0 > cut) t1 = t0 + ((t1 - t0) / cut) * cut;
     stages.push_back(t1);
     t0 = t1;
   }
@@ -1333,9 +1338,7 @@ bool plan_tx(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>&
   f->h_lx_stage = stages;
   f->lx_stage_cap = static_cast<int64_t>(cap);
   const double per_stage = static_cast<double>(T) / static_cast<double>(stages.size() - 1);
-  f->lx_ilp = per_stage >= 7.5 ? 8 : per_stage >= 6.5 ? 7 : 4;
-  const int force_ilp = env_int("TI_LX_ILP", 0);
-  if (force_ilp > 0) f->lx_ilp = force_ilp >= 8 ? 8 : force_ilp == 7 ? 7 : 4;
+  f->lx_ilp = cut ? cut : per_stage >= 7.5 ? 8 : per_stage >= 6.5 ? 7 : 4;
   f->hx_top = D0;
   f->layout = 9;
   return true;
