@@ -206,3 +206,29 @@ def test_matrix_chunks_concatenate_and_fan_out():
     assert [x["predictions"] for x in mixed] == [[2.0], [11.0], [4.0] * 4]
     with pytest.raises(Exception):
         run(Batcher(predict_batch).submit(np.zeros((0, 3))))
+
+
+def test_enqueue_futures_resolve_like_submit():
+    """Batcher.enqueue (submit without the coroutine, bench.py's load): the
+    futures resolve with the same per-request slices and one batchId, and an
+    empty request raises at once."""
+    import numpy as np
+
+    async def main():
+        b, calls = echo_batcher(max_batch_size=7, max_latency_ms=50)
+        got = {}
+        futs = []
+        for i, n in enumerate([3, 2, 2]):
+            f = b.enqueue(np.full((n, 2), float(i), dtype=np.float32))
+            f.add_done_callback(lambda fut, i=i: got.__setitem__(i, fut.result()))
+            futs.append(f)
+        await asyncio.gather(*futs)
+        with pytest.raises(HTTPError):
+            b.enqueue(np.zeros((0, 2), dtype=np.float32))
+        return got, calls
+    got, calls = run(main())
+    assert len(calls) == 1 and len(calls[0]) == 7            # one batch of 7 rows
+    assert len({r["batchId"] for r in got.values()}) == 1
+    for i, n in enumerate([3, 2, 2]):
+        assert np.asarray(got[i]["predictions"]).shape == (n, 2)
+        assert np.all(np.asarray(got[i]["predictions"]) == float(i))
