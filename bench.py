@@ -9,21 +9,20 @@ collective ("weak": every rank predicts its own 1M rows); value = all ranks'
 rows / max-over-ranks wall time.
 
 Also reported (rank 0):
-  roofline     -- the resource that binds the C2 kernel: VALU issue (DESIGN.md
-                  4).  achieved = VALU wave-instructions per launch (committed
-                  rocprofv3 PMC pass of the same kernel, profiles/pmc_c2.json)
-                  / the kernel's average duration from HIP events on the launch
-                  stream; peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64
-                  VALU instruction (MI355X_MICROARCH.md: a wave64 VALU
-                  instruction issues over 2 cycles on a SIMD-32).  Beside it:
-                  `peak_mix`, the ceiling of the walk's own instruction mix
-                  measured by scripts/micro/valu_rate.hip at the chip's
-                  effective clock (profiles/r3_valu_rate.jsonl), and
-                  `profiled`, the same count priced on the PMC run's own
-                  cycles (GRBM_GUI_ACTIVE per XCD; its clock = those cycles /
-                  its kernel duration).  The HBM view is kept beside it:
-                  compulsory bytes (X + out) and counter bytes (FETCH_SIZE x 2
-                  + WRITE_SIZE) per launch as fractions of 8 TB/s.
+  roofline     -- the resource that binds the C2 kernel:
+                  the busiest of VALU issue, the LDS array and the TD in the
+                  committed rocprofv3 PMC pass of the same kernel
+                  (profiles/pmc_c2.json), priced on that pass's own cycles
+                  (GRBM_GUI_ACTIVE per XCD): the LDS array, ~0.74.  `valu`
+                  keeps the VALU view: achieved = VALU wave-instructions per
+                  launch / the kernel's average duration from HIP events on
+                  the launch stream; peak = 1,024 SIMDs x 2.4 GHz / 2 cycles
+                  per wave64 instruction (MI355X_MICROARCH.md); `peak_mix`,
+                  the ceiling of the walk's own instruction mix measured by
+                  scripts/micro/valu_rate.hip (profiles/r3_valu_rate.jsonl).
+                  The HBM view is kept beside it: compulsory bytes (X + out)
+                  and counter bytes (FETCH_SIZE x 2 + WRITE_SIZE) per launch
+                  as fractions of 8 TB/s.
   cpu_baseline -- the C/OpenMP restatement of xgboost 0.82's predict loop
                   (oracle/c/tree_port.c, kind "port": xgboost is not installed)
                   timed on this host on a bounded sample of the same rows.
@@ -194,7 +193,14 @@ def load_pmc(path: str):
 
 
 def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str, step_op: str = None):
-    """Binding-resource roofline of the C2 kernel (see the module docstring)."""
+    """Roofline of the C2 kernel (see the module docstring): the busiest of
+    the issue resources the committed PMC pass of the same kernel counts --
+    VALU issue, the LDS array, the TD -- each priced on that pass's own
+    cycles, as config_roofline does for C3 / C4.  `bound` / `frac` are the
+    busiest; `achieved` / `peak` are in that resource's unit (LDS-array and TD
+    cycles per second per CU against the 2.4 GHz clock; VALU wave64
+    instructions per second against the 2-cycle issue peak).  The VALU view,
+    the step-mix ceiling and the HBM view stay beside it."""
     pmc = load_pmc(pmc_path)
     if pmc and not (pmc.get("rows") == rows and pmc.get("workload") == "c2"
                     and pmc.get("layout") == layout and "valu_insts_per_launch" in pmc
@@ -208,35 +214,54 @@ def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str, step_op: s
                          "wave64 VALU instruction (MI355X_MICROARCH.md)",
            "hbm_compulsory_bytes": compulsory,
            "hbm_compulsory_frac": compulsory / t / HBM_PEAK}
-    if pmc:
-        valu = pmc["valu_insts_per_launch"]
-        out["achieved"] = valu / t / 1e9
-        out["frac"] = valu / t / VALU_PEAK
-        out["valu_insts_per_launch"] = valu
-        out["traffic"] = pmc.get("hbm_bytes_per_launch")
-        if out["traffic"]:
-            out["hbm_counter_frac"] = out["traffic"] / t / HBM_PEAK
-            out["traffic_over_compulsory"] = out["traffic"] / (compulsory + pmc.get(
-                "model_bytes", 0))
-        cyc = pmc.get("gui_active_cycles_per_xcd")
-        if cyc:
-            out["profiled"] = {
-                "frac": valu * VALU_CYCLES / (SIMDS * cyc),
-                "kernel_ms": (pmc.get("profiled_kernel_ns") or 0) * 1e-6 or None,
-                "clock_GHz": pmc.get("profiled_clock_GHz"),
-                "basis": "VALU x 2 cycles / (1,024 SIMDs x GRBM_GUI_ACTIVE/8 of the PMC pass)"}
-        out["pmc_source"] = pmc.get("source")
+    if not pmc:
+        return out
+    valu = pmc["valu_insts_per_launch"]
+    cfg = config_roofline(kernel_ms, rows, layout, "c2", pmc_path) or {}
+    fr = cfg.get("fracs") or {}
+    valu_view = {"achieved": valu / t / 1e9, "peak": VALU_PEAK / 1e9, "unit": "Ginst/s",
+                 "frac": valu / t / VALU_PEAK, "valu_insts_per_launch": valu,
+                 "peak_basis": out["peak_basis"]}
+    cyc = pmc.get("gui_active_cycles_per_xcd")
+    if cyc:
+        valu_view["profiled"] = {
+            "frac": valu * VALU_CYCLES / (SIMDS * cyc),
+            "kernel_ms": (pmc.get("profiled_kernel_ns") or 0) * 1e-6 or None,
+            "clock_GHz": pmc.get("profiled_clock_GHz"),
+            "basis": "VALU x 2 cycles / (1,024 SIMDs x GRBM_GUI_ACTIVE/8 of the PMC pass)"}
     if step_op:
         st = valu_step_rate(step_op)
         if st:
             mix = st["valu_per_step"] / st["cycles_per_step_per_simd"] * SIMDS * CLOCK_HZ
-            out["peak_mix"] = mix / 1e9
-            out["peak_mix_basis"] = (f"walk step '{st['op']}': {st['valu_per_step']} VALU in "
-                                     f"{st['cycles_per_step_per_simd']:.2f} cycles per SIMD at 8 "
-                                     f"waves/SIMD (profiles/r3_valu_rate.jsonl), x {SIMDS} SIMDs "
-                                     f"x {CLOCK_HZ / 1e9} GHz")
-            if out["achieved"]:
-                out["frac_mix"] = out["achieved"] * 1e9 / mix
+            valu_view["peak_mix"] = mix / 1e9
+            valu_view["frac_mix"] = valu / t / mix
+            valu_view["peak_mix_basis"] = (
+                f"walk step '{st['op']}': {st['valu_per_step']} VALU in "
+                f"{st['cycles_per_step_per_simd']:.2f} cycles per SIMD at 8 waves/SIMD "
+                f"(profiles/r3_valu_rate.jsonl), x {SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz")
+    out["valu"] = valu_view
+    out["fracs"] = fr
+    out["fracs_bench"] = cfg.get("fracs_bench")
+    bound = cfg.get("bound", "valu_issue")
+    out["bound"] = bound
+    out["frac"] = fr.get(bound, valu_view["frac"])
+    if bound == "valu_issue":
+        out.update(achieved=valu_view["achieved"], peak=valu_view["peak"], unit="Ginst/s")
+    else:
+        # busy cycles per CU per second of the profiled run (achieved / peak =
+        # the busy fraction of the PMC pass's own cycles)
+        out.update(achieved=out["frac"] * CLOCK_HZ / 1e9, peak=CLOCK_HZ / 1e9,
+                   unit=f"G {bound} cycles/s per CU",
+                   peak_basis=f"one {bound} cycle per clock per CU at {CLOCK_HZ / 1e9} GHz; frac "
+                              "priced on the PMC pass's own cycles (GRBM_GUI_ACTIVE per XCD)")
+    for k in ("lds_bank_conflict_frac", "wait_frac", "l2_hit_rate", "waves_per_simd"):
+        if pmc.get(k) is not None:
+            out[k] = pmc[k]
+    out["traffic"] = pmc.get("hbm_bytes_per_launch")
+    if out["traffic"]:
+        out["hbm_counter_frac"] = out["traffic"] / t / HBM_PEAK
+        out["traffic_over_compulsory"] = out["traffic"] / (compulsory + pmc.get("model_bytes", 0))
+    out["pmc_source"] = pmc.get("source")
     return out
 
 

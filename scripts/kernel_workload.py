@@ -39,6 +39,8 @@ def main():
     p.add_argument("--workload", required=True)
     p.add_argument("--rows", type=int, default=1_000_000)
     p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--x-buffers", type=int, default=1,
+                   help="copies of the batch the launches rotate through (bench.py uses 3 for C2)")
     a = p.parse_args()
     import torch
     import bench
@@ -46,13 +48,17 @@ def main():
     from kfserving_amd.forest import OUT_PREDICT, TI_F32, TI_F64
     forest, F, dtype = forest_of(a.workload)
     dev = DeviceForest(forest, [0])
-    X = bench.device_normal(a.rows, F, 3, "cuda:0", dtype)
+    Xs = [bench.device_normal(a.rows, F, 3, "cuda:0", dtype)]
+    Xs += [Xs[0].clone() for _ in range(max(0, a.x_buffers - 1))]
+    it = [0]
     xdt = TI_F64 if dtype == "float64" else TI_F32
     out = torch.empty(a.rows * forest.output_width(OUT_PREDICT),
                       dtype=torch.float64 if forest.accum_dtype else torch.float32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
 
     def step():
+        X = Xs[it[0] % len(Xs)]
+        it[0] += 1
         dev.predict_device(X.data_ptr(), xdt, a.rows, F, F, OUT_PREDICT, out.data_ptr(),
                            out.numel(), stream=sh)
     step()
