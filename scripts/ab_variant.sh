@@ -1,9 +1,18 @@
-cd "$GRAFT_REPO_ROOT"
-V=$GRAFT_REPO_ROOT/kfserving_amd/lib/variants/nt0/libtreeinfer.so
+#!/bin/bash
+# A/B of the in-tree library against a variant build (TREEINFER_LIB) on the
+# kernel workloads of scripts/kernel_workload.py, interleaved, two rounds.
+# Build the variant with extra -D flags into kfserving_amd/lib/variants/NAME/
+# (git-ignored), then: scripts/ab_variant.sh NAME OUT_SUBDIR [workloads...]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+V=$(pwd)/kfserving_amd/lib/variants/$1/libtreeinfer.so
+OUT=gpurun_out/$2
+shift 2
+mkdir -p "$OUT"
+WL=${*:-c2 c3 c3_maxbin c4}
 for rep in 1 2; do
-for w in c2 c3 c3_maxbin c4; do
-  xb=1; [ $w = c2 ] && xb=3
-  timeout -k 10 120 python scripts/kernel_workload.py --workload $w --steps 10 --x-buffers $xb | sed "s/}/, \"nt\": 1}/" >> gpurun_out/r3s/ab.jsonl || exit 1
-  TREEINFER_LIB=$V timeout -k 10 120 python scripts/kernel_workload.py --workload $w --steps 10 --x-buffers $xb | sed "s/}/, \"nt\": 0}/" >> gpurun_out/r3s/ab.jsonl || exit 1
-done; done
-cd /tmp && export TMPDIR=/tmp && timeout -k 10 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $GRAFT_REPO_ROOT/gpurun_out/r3s/fetch_nt1 -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/kernel_workload.py --workload c2 --steps 6 --x-buffers 3 > $GRAFT_REPO_ROOT/gpurun_out/r3s/fetch_nt1.log 2>&1
+  for w in $WL; do
+    xb=1; [ "$w" = c2 ] && xb=3
+    timeout -k 10 120 python scripts/kernel_workload.py --workload $w --steps 10 --x-buffers $xb | sed "s/}/, \"variant\": 0}/" >> $OUT/ab.jsonl || exit 1
+    TREEINFER_LIB=$V timeout -k 10 120 python scripts/kernel_workload.py --workload $w --steps 10 --x-buffers $xb | sed "s/}/, \"variant\": 1}/" >> $OUT/ab.jsonl || exit 1
+  done
+done
