@@ -1820,6 +1820,24 @@ int ensure_lds_attr(int device, KernelFn fn) {
   return TI_OK;
 }
 
+// TI_OCC=1: print, once per kernel, the workgroups per CU the runtime's
+// occupancy calculator allows for this launch shape (a diagnostic for the
+// PMC passes' resident-wave counts).
+void occ_note(KernelFn fn, int block, size_t lds) {
+  static const int on = env_int("TI_OCC", 0);
+  if (!on) return;
+  static std::mutex mu;
+  static std::set<const void*> seen;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!seen.insert(reinterpret_cast<const void*>(fn)).second) return;
+  int n = -1;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), block, lds);
+  hipFuncAttributes attr;
+  (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(fn));
+  std::fprintf(stderr, "[ti occupancy] block %d lds %zu B: %d workgroups/CU (%d waves/SIMD), %d VGPRs, %d SGPRs\n",
+               block, lds, n, n * ((block + 63) / 64) / 4, attr.numRegs, 0);
+}
+
 int64_t output_width(const ti_forest* f, int kind) {
   if (kind == TI_OUTPUT_LEAF) return f->T;
   if (kind == TI_OUTPUT_CONTRIB) return static_cast<int64_t>(f->K) * (f->F + 1);
@@ -1981,7 +1999,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    occ_note(fn, R, lds);
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
   } else if (f->layout == 6) {
@@ -2004,7 +2023,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    occ_note(fn, R, lds);
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
   } else if (f->layout == 7) {
@@ -2033,7 +2053,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    occ_note(fn, R, lds);
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
   } else if (f->layout == 9) {
@@ -2066,7 +2087,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    occ_note(fn, R, lds);
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
   } else if (f->layout == 8) {
@@ -2097,7 +2119,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    occ_note(fn, R, lds);
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
   } else {
@@ -2115,6 +2138,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   if (rc) return rc;
   const int64_t grid = (rows + R - 1) / R;
   if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
+  occ_note(fn, R, lds);
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
   TI_HIP(hipGetLastError());
   return TI_OK;
