@@ -162,17 +162,24 @@ __constant__ ShapInvTable kShapInv = make_inv(std::make_integer_sequence<int, 65
 // or the 1/k table.  The row's contributions accumulate in LDS [W][64]
 // (W = K * (F + 1) <= kShapLdsW), so no global read-modify-write.
 constexpr int kShapLdsW = 128;
+constexpr int kShapTabStride = 8;   // coefficients per one-pattern in the table (paths of <= 8 elements)
 constexpr int64_t kShapWaveTarget = 65536;        // 64-row waves per contrib launch (sweep: profiles/r1_shap_sweep.log)
 constexpr int64_t kShapMinPathsPerSlice = 256;
 constexpr int64_t kShapMaxSlices = 64;
 constexpr uint64_t kShapPartBytesMax = 2ull << 30;
-template <typename XT, typename ACC, typename MT, int MAXN>
+// TAB: the per-element coefficients UnwoundPathSum x (one - zero) of every
+// path and every pattern of one fractions were computed once per forest
+// (shap_table_kernel, the same expressions in the same MT arithmetic), so a
+// path costs its n element tests, n coefficient loads at [path][om] and the
+// n accumulations, instead of the O(n^2) extend and unwind: the same floats.
+template <typename XT, typename ACC, typename MT, int MAXN, bool TAB = false>
 __global__ void __launch_bounds__(64) contrib_reg_kernel(
     const XT* __restrict__ X, int64_t rows, int64_t stride, int32_t cols, int32_t zero_map_on,
     const ShapPath* __restrict__ paths, int64_t n_paths, const ShapElem* __restrict__ elems,
     const double* __restrict__ leafv, int32_t LW, int32_t K, int32_t F, int32_t maxl,
     const double* __restrict__ bias, double divisor, double* __restrict__ part,
-    int64_t paths_per_slice, ACC* __restrict__ out) {
+    int64_t paths_per_slice, ACC* __restrict__ out, const MT* __restrict__ tab,
+    const int64_t* __restrict__ tab_off) {
   (void)maxl;
   extern __shared__ double shap_lds[];
   const int lane = threadIdx.x;
@@ -198,6 +205,35 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
       else if (x == 0.0) follow = (e.flags & kShapZeroOk) != 0;
       else follow = !(e.flags & kShapEmpty) && e.lo < x && x <= e.hi;
       om |= (follow ? 1u : 0u) << i;
+    }
+    if constexpr (TAB) {
+      // the pattern's coefficients: kShapTabStride values, 32- or 64-byte
+      // aligned, read with whole-vector loads (a lane touches one line)
+      typedef MT v4_t __attribute__((ext_vector_type(4)));
+      const v4_t* c4 = reinterpret_cast<const v4_t*>(tab + tab_off[p] + (int64_t)om * kShapTabStride);
+      MT c[kShapTabStride];
+#pragma unroll
+      for (int j = 0; j < kShapTabStride / 4; ++j) {
+        const v4_t v = c4[j];
+        c[4 * j] = v.x;
+        c[4 * j + 1] = v.y;
+        c[4 * j + 2] = v.z;
+        c[4 * j + 3] = v.w;
+      }
+      const double* lv = leafv + P.leaf * LW;
+      if (LW == 1) {
+        const MT l0 = static_cast<MT>(lv[0]);
+#pragma unroll
+        for (int e_i = 0; e_i < kShapTabStride; ++e_i)
+          if (e_i < n) phi[(P.group * (F + 1) + pe[e_i].feature) * 64] += c[e_i] * l0;
+      } else {
+#pragma unroll
+        for (int e_i = 0; e_i < kShapTabStride; ++e_i)
+          if (e_i < n)
+            for (int k = 0; k < LW; ++k)
+              phi[(k * (F + 1) + pe[e_i].feature) * 64] += c[e_i] * static_cast<MT>(lv[k]);
+      }
+      continue;
     }
     // ExtendPath from scratch
     MT w[MAXN + 1];
@@ -307,6 +343,85 @@ __global__ void __launch_bounds__(64) contrib_reg_kernel(
     for (int f = 0; f < F; ++f)
       o[g * (F + 1) + f] = (ACC)(static_cast<double>(phi[(g * (F + 1) + f) * 64]) / divisor);
     o[g * (F + 1) + F] = (ACC)bias[g];
+  }
+}
+
+// The coefficient table of contrib_reg_kernel<TAB>: one workgroup per path,
+// a lane per pattern om of one fractions (bit i = element i followed): the
+// path weights extended from scratch and, per element, UnwoundPathSum x
+// (one - zero) -- the expressions of contrib_reg_kernel in the same order
+// and type, so the table holds the floats the kernel would compute.
+template <typename MT, int MAXN>
+__global__ void __launch_bounds__(256) shap_table_kernel(const ShapPath* __restrict__ paths,
+                                                         const ShapElem* __restrict__ elems,
+                                                         const int64_t* __restrict__ tab_off,
+                                                         MT* __restrict__ tab) {
+  const ShapPath P = paths[blockIdx.x];
+  const int n = P.n;
+  const ShapElem* pe = elems + P.first;
+  MT* out = tab + tab_off[blockIdx.x];
+  for (uint32_t om = threadIdx.x; om < (1u << n); om += blockDim.x) {
+    MT w[MAXN + 1];
+    w[0] = MT(1);
+#pragma unroll
+    for (int d = 1; d <= MAXN; ++d) {
+      if (d <= n) {
+        const MT of = ((om >> (d - 1)) & 1u) ? MT(1) : MT(0);
+        const MT zf = static_cast<MT>(pe[d - 1].zf);
+        w[d] = MT(0);
+#pragma unroll
+        for (int i = d - 1; i >= 0; --i) {
+          w[i + 1] += of * w[i] * static_cast<MT>((double)(i + 1) / (double)(d + 1));
+          w[i] = zf * w[i] * static_cast<MT>((double)(d - i) / (double)(d + 1));
+        }
+      }
+    }
+    const MT rn1 = static_cast<MT>(n + 1);
+    const MT in1 = static_cast<MT>(kShapInv.v[n + 1]);
+    MT wn = MT(0);
+#pragma unroll
+    for (int i = 0; i <= MAXN; ++i)
+      if (i == n) wn = w[i];
+    for (int e_i = 0; e_i < n; ++e_i) {
+      const bool one = ((om >> e_i) & 1u) != 0u;
+      const MT zf = static_cast<MT>(pe[e_i].zf);
+      MT total;
+      if constexpr (std::is_same<MT, float>::value) {
+        // contrib_reg_kernel's packed float path: both sums, then the select
+        const float izf = 1.0f / zf;
+        float next = wn, tot1 = 0.0f, tot0 = 0.0f;
+#pragma unroll
+        for (int i = MAXN - 1; i >= 0; --i) {
+          if (i < n) {
+            const float tmp = next * (rn1 * static_cast<float>(1.0 / (double)(i + 1)));
+            tot1 += tmp;
+            next = w[i] - tmp * zf * (static_cast<float>(n - i) * in1);
+            tot0 += w[i] * izf * (rn1 * static_cast<float>(kShapInv.v[n - i]));
+          }
+        }
+        total = one ? tot1 : tot0;
+      } else {
+        total = MT(0);
+        if (one) {
+          MT next = wn;
+#pragma unroll
+          for (int i = MAXN - 1; i >= 0; --i) {
+            if (i < n) {
+              const MT tmp = next * (rn1 * static_cast<MT>(1.0 / (double)(i + 1)));
+              total += tmp;
+              next = w[i] - tmp * zf * (static_cast<MT>(n - i) * in1);
+            }
+          }
+        } else {
+          const MT izf = MT(1) / zf;
+#pragma unroll
+          for (int i = MAXN - 1; i >= 0; --i) {
+            if (i < n) total += w[i] * izf * (rn1 * static_cast<MT>(kShapInv.v[n - i]));
+          }
+        }
+      }
+      out[(int64_t)om * kShapTabStride + e_i] = total * ((one ? MT(1) : MT(0)) - zf);
+    }
   }
 }
 
@@ -425,6 +540,8 @@ struct DeviceForest {
   ShapElem* shap_elems = nullptr;
   double* shap_leaf = nullptr;
   double* shap_bias = nullptr;
+  void* shap_tab = nullptr;          // TreeSHAP coefficient table (shap_table_kernel), MT-typed
+  int64_t* shap_tab_off = nullptr;   // [paths] first coefficient of each path
   // ti_predict scratch: device buffers + pinned host staging (grown x2)
   void* x_buf = nullptr;
   size_t x_cap = 0;
@@ -526,6 +643,11 @@ struct ti_forest {
   };
   std::unique_ptr<ShapSource> shap_src;
   std::vector<ShapPath> h_paths;
+  // TreeSHAP coefficient table: per path, (2^n one-patterns) x n coefficients
+  // (contrib_reg_kernel TAB); shap_tab_mt = 4 / 8 bytes per coefficient, 0: none
+  int32_t shap_tab_mt = 0;
+  std::vector<int64_t> h_tab_off;
+  int64_t shap_tab_len = 0;
   std::vector<ShapElem> h_elems;
   std::vector<double> h_path_leaf, h_shap_bias;
   // host images (kept until upload)
@@ -561,7 +683,7 @@ void free_device(DeviceForest& d) {
                   d.leaf_base, d.leaves, d.exp_leaf_ids, d.tree_group, d.x_buf, d.out_buf,
                   d.cat_words, d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1],
                   d.bx_tbl[0], d.bx_tbl[1],
-                  d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias,
+                  d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias, d.shap_tab, d.shap_tab_off,
                   d.rx_recs[0], d.rx_recs[1], d.rx_base, d.rx_nint, d.lx_stage,
                   d.tx8_pos, d.tx8_val, d.tx8_ord,
                   d.hx_top[0], d.hx_top[1]};
@@ -600,6 +722,8 @@ void free_device(DeviceForest& d) {
   d.shap_paths = nullptr;
   d.shap_elems = nullptr;
   d.shap_leaf = d.shap_bias = nullptr;
+  d.shap_tab = nullptr;
+  d.shap_tab_off = nullptr;
   d.x_cap = d.out_cap = 0;
   d.stream = nullptr;
   d.device = -1;
@@ -2444,6 +2568,26 @@ int ensure_shap(ti_forest* f) {
   std::lock_guard<std::mutex> lk(f->shap_mu);
   if (f->shap_ready.load(std::memory_order_relaxed)) return TI_OK;
   build_shap(&f->shap_src->desc, f);
+  // the coefficient table (contrib_reg_kernel TAB): paths of <= 8 unique
+  // features, 2^n x 8 coefficients each (padded), in the path arithmetic's type;
+  // built when the whole table stays under TI_SHAP_TABLE_MB (2048; 0: never)
+  {
+    static const int table_mb = env_int("TI_SHAP_TABLE_MB", 2048);
+    static const int force_f64 = env_int("TI_SHAP_F64", 0);
+    const int mt = (f->accum != TI_F64 && !force_f64) ? 4 : 8;
+    const int64_t W = static_cast<int64_t>(f->K) * (f->F + 1);
+    f->h_tab_off.assign(f->h_paths.size(), 0);
+    int64_t len = 0;
+    bool ok = table_mb > 0 && W <= kShapLdsW && f->shap_maxl <= kShapTabStride;
+    for (size_t i = 0; ok && i < f->h_paths.size(); ++i) {
+      f->h_tab_off[i] = len;
+      len += (int64_t(1) << f->h_paths[i].n) * kShapTabStride;
+      ok = len * mt <= static_cast<int64_t>(table_mb) << 20;
+    }
+    f->shap_tab_mt = ok && !f->h_paths.empty() ? mt : 0;
+    f->shap_tab_len = f->shap_tab_mt ? len : 0;
+    if (!f->shap_tab_mt) f->h_tab_off.clear();
+  }
   int dev0 = 0;
   TI_HIP(hipGetDevice(&dev0));
   int rc = TI_OK;
@@ -2455,6 +2599,21 @@ int ensure_shap(ti_forest* f) {
         (rc = upload(&d.shap_leaf, f->h_path_leaf, &d.bytes)) ||
         (rc = upload(&d.shap_bias, f->h_shap_bias, &d.bytes)))
       break;
+    if (f->shap_tab_mt) {
+      if ((rc = upload(&d.shap_tab_off, f->h_tab_off, &d.bytes))) break;
+      const size_t bytes = static_cast<size_t>(f->shap_tab_len) * f->shap_tab_mt;
+      TI_HIP(hipMalloc(&d.shap_tab, std::max<size_t>(bytes, 16)));
+      d.bytes += static_cast<int64_t>(bytes);
+      const unsigned np = static_cast<unsigned>(f->h_paths.size());
+      if (f->shap_tab_mt == 4)
+        hipLaunchKernelGGL((shap_table_kernel<float, 16>), dim3(np), dim3(256), 0, nullptr,
+                           d.shap_paths, d.shap_elems, d.shap_tab_off, static_cast<float*>(d.shap_tab));
+      else
+        hipLaunchKernelGGL((shap_table_kernel<double, 16>), dim3(np), dim3(256), 0, nullptr,
+                           d.shap_paths, d.shap_elems, d.shap_tab_off, static_cast<double*>(d.shap_tab));
+      TI_HIP(hipGetLastError());
+      TI_HIP(hipDeviceSynchronize());
+    }
   }
   TI_HIP(hipSetDevice(dev0));
   if (rc) return rc;
@@ -2497,19 +2656,37 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
     while (slices > 1 && static_cast<uint64_t>(slices) * W * rows * 8 > kShapPartBytesMax) --slices;
     slices = std::max<int64_t>(slices, 1);
     const int64_t pps = (n_paths + slices - 1) / slices;
+    // the coefficient table pays off for small batches (C2 model: 4,096 rows
+    // 4.1e5 vs 2.7e5 rows/s); at 100k rows its gathers (a 64-row wave reads
+    // most of each path's 2^n x 32 B block) make it slower than the extend /
+    // unwind arithmetic (2.2e5 vs 2.9e5): profiles/r3_shap_table.jsonl
+    static const int64_t tab_rows = env_int("TI_SHAP_TABLE_ROWS", 16384);
     double* part = nullptr;
     if (slices > 1)
       TI_HIP(hipMallocAsync(reinterpret_cast<void**>(&part),
                             static_cast<size_t>(slices * W * rows) * 8, stream));
 #define TI_CONTRIB_REG(XT_, ACC_, MT_, N_)                                                          \
   do {                                                                                         \
-    int rc_ = ensure_lds_attr(d.device, reinterpret_cast<KernelFn>(contrib_reg_kernel<XT_, ACC_, MT_, N_>)); \
+    const bool tab_ = d.shap_tab != nullptr && f->shap_tab_mt == (int)sizeof(MT_) &&           \
+                      rows <= tab_rows;                                                        \
+    KernelFn fn_ = tab_ ? reinterpret_cast<KernelFn>(contrib_reg_kernel<XT_, ACC_, MT_, 8, true>) \
+                        : reinterpret_cast<KernelFn>(contrib_reg_kernel<XT_, ACC_, MT_, N_>);  \
+    int rc_ = ensure_lds_attr(d.device, fn_);                                                  \
     if (rc_) return rc_;                                                                       \
-    hipLaunchKernelGGL((contrib_reg_kernel<XT_, ACC_, MT_, N_>), dim3(grid_r, (unsigned)slices), dim3(64), \
-                       lds_w, stream,                                                          \
-                       static_cast<const XT_*>(X), rows, stride, cols, f->lgb_zero_map,        \
-                       d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,    \
-                       f->shap_maxl, d.shap_bias, f->divisor, part, pps, static_cast<ACC_*>(out)); \
+    if (tab_)                                                                                  \
+      hipLaunchKernelGGL((contrib_reg_kernel<XT_, ACC_, MT_, 8, true>), dim3(grid_r, (unsigned)slices), \
+                         dim3(64), lds_w, stream,                                              \
+                         static_cast<const XT_*>(X), rows, stride, cols, f->lgb_zero_map,      \
+                         d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,  \
+                         f->shap_maxl, d.shap_bias, f->divisor, part, pps, static_cast<ACC_*>(out), \
+                         static_cast<const MT_*>(d.shap_tab), d.shap_tab_off);                 \
+    else                                                                                       \
+      hipLaunchKernelGGL((contrib_reg_kernel<XT_, ACC_, MT_, N_>), dim3(grid_r, (unsigned)slices), dim3(64), \
+                         lds_w, stream,                                                        \
+                         static_cast<const XT_*>(X), rows, stride, cols, f->lgb_zero_map,      \
+                         d.shap_paths, n_paths, d.shap_elems, d.shap_leaf, f->LW, f->K, f->F,  \
+                         f->shap_maxl, d.shap_bias, f->divisor, part, pps, static_cast<ACC_*>(out), \
+                         static_cast<const MT_*>(nullptr), static_cast<const int64_t*>(nullptr)); \
     if (part) {                                                                                \
       const unsigned g2 = static_cast<unsigned>((rows + 255) / 256);                           \
       hipLaunchKernelGGL((contrib_slices_kernel<ACC_>), dim3(g2), dim3(256), 0, stream, part,  \
