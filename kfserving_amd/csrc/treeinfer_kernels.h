@@ -880,18 +880,77 @@ __device__ __forceinline__ uint32_t lds_u32(uint32_t byte_addr) {
       static_cast<uintptr_t>(byte_addr));
 }
 
+#ifndef TI_FIX_SROOT
+#define TI_FIX_SROOT 1
+#endif
+// SROOT: the root and its children pair are the same for every lane, so words
+// 0..3 of each tree's image come as scalar loads from global memory, issued
+// between the two barriers of the stage commit (whose LDS wait covers their
+// latency; a scalar load still in flight would make every LDS wait of the walk
+// wait for it), and level 0 is the bin read, a compare against the scalar rank
+// and a select between two scalars: no pair read from LDS.  C2 0.787 -> 0.775
+// ms (profiles/r3_c2_sroot_ab.jsonl); level 1's pair selected from the four
+// scalars of level 2 by level 0's decision was 5 % slower (its VALU selects
+// cost more than the LDS read they replace).
+typedef const __attribute__((address_space(4))) u32x4 fix_cu4_t;
+template <int NG>
+__device__ __forceinline__ void fix_tops(const KArgs& a, int t0, u32x4 (&top)[4 * NG]) {
+  fix_cu4_t* timg = reinterpret_cast<fix_cu4_t*>(reinterpret_cast<uintptr_t>(a.trees));
+#pragma unroll
+  for (int i = 0; i < 4 * NG; ++i) top[i] = timg[min(t0 + i, a.n_trees - 1) * (kFixTree / 16)];
+}
+template <bool B16, bool CHECK_NAN>
+__device__ __forceinline__ void fix_step(uint32_t& nd, uint32_t b, uint2 pr) {
+  if (!CHECK_NAN) {
+    asm("v_cmp_lt_u32_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_cndmask_b32 %0, %2, %3, vcc"
+        : "+v"(nd) : "v"(b), "v"(pr.x), "v"(pr.y) : "vcc");
+  } else {
+    // right = (rank < bin) && !(bin == NaN code && NaN-left (bit 15))
+    uint64_t mn, ml;
+    asm("v_cmp_lt_u32_sdwa vcc, %0, %3 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_cmp_eq_u32_e64 %1, %6, %3\n\t"
+        "v_cmp_gt_i16_e64 %2, 0, %0\n\t"
+        "s_and_b64 %1, %1, %2\n\t"
+        "s_andn2_b64 vcc, vcc, %1\n\t"
+        "v_cndmask_b32 %0, %4, %5, vcc"
+        : "+v"(nd), "=&s"(mn), "=&s"(ml)
+        : "v"(b), "v"(pr.x), "v"(pr.y), "s"(BinTraits<B16>::kNan)
+        : "vcc", "scc");
+  }
+}
 template <int KMAX, bool B16, bool CHECK_NAN, int NG>
 __device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0, float (&acc)[KMAX],
-                                                uint32_t lane_off) {
+                                                uint32_t lane_off, const u32x4 (&top)[4 * NG]) {
   const uint32_t bmask = a.bin_mask;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     if (g * 4 >= cnt) break;   // uniform: the last stage may be short
     uint32_t nd[4];
+#if TI_FIX_SROOT
+    {
+      uint32_t b0[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b0[q] = lds_bin<B16>((top[g * 4 + q].y & bmask) | lane_off);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const u32x4 tp = top[g * 4 + q];
+        // v_cmp against the scalar rank, two v_mov and a v_cndmask (with vcc
+        // as the mask, gfx9's constant bus takes no SGPR source besides it)
+        bool right = (tp.y >> 16) < b0[q];
+        if (CHECK_NAN && (tp.y & 0x8000u)) right = right && b0[q] != BinTraits<B16>::kNan;
+        nd[q] = right ? tp.w : tp.z;
+      }
+    }
+    constexpr int l_first = 1;
+#else
+    (void)top;
 #pragma unroll
     for (int q = 0; q < 4; ++q) nd[q] = lds_u32(kFixStage + (uint32_t)((g * 4 + q) * kFixTree) + 4u);
+    constexpr int l_first = 0;
+#endif
 #pragma unroll
-    for (int l = 0; l < 8; ++l) {
+    for (int l = l_first; l < 8; ++l) {
       uint32_t b[4];
       uint2 pr[4];
 #pragma unroll
@@ -900,25 +959,7 @@ __device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0,
         pr[q] = lds_u2c((nd[q] & kBNodePairMask) + (kFixStage + (uint32_t)((g * 4 + q) * kFixTree)));
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!CHECK_NAN) {
-          asm("v_cmp_lt_u32_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:DWORD\n\t"
-              "v_cndmask_b32 %0, %2, %3, vcc"
-              : "+v"(nd[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y) : "vcc");
-        } else {
-          // right = (rank < bin) && !(bin == NaN code && NaN-left (bit 15))
-          uint64_t mn, ml;
-          asm("v_cmp_lt_u32_sdwa vcc, %0, %3 src0_sel:WORD_1 src1_sel:DWORD\n\t"
-              "v_cmp_eq_u32_e64 %1, %6, %3\n\t"
-              "v_cmp_gt_i16_e64 %2, 0, %0\n\t"
-              "s_and_b64 %1, %1, %2\n\t"
-              "s_andn2_b64 vcc, vcc, %1\n\t"
-              "v_cndmask_b32 %0, %4, %5, vcc"
-              : "+v"(nd[q]), "=&s"(mn), "=&s"(ml)
-              : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y), "s"(BinTraits<B16>::kNan)
-              : "vcc", "scc");
-        }
-      }
+      for (int q = 0; q < 4; ++q) fix_step<B16, CHECK_NAN>(nd[q], b[q], pr[q]);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -960,9 +1001,13 @@ __global__ void __launch_bounds__(512) bheap_fix_kernel(const KArgs a) {
       flag, reinterpret_cast<XT*>(smem + kFixStage), a, row0, R, tid);
   float acc[KMAX];
   init_acc(acc, a);
+  u32x4 top[4 * NG] = {};
   for (int t0 = 0; t0 < T; t0 += S) {
     const int cnt = (T - t0) < S ? (T - t0) : S;
     __syncthreads();
+#if TI_FIX_SROOT
+    fix_tops<NG>(a, t0, top);
+#endif
 #pragma unroll
     for (int u = 0; u < NG; ++u) stage[tid + u * R] = pf[u];
     __syncthreads();
@@ -975,9 +1020,9 @@ __global__ void __launch_bounds__(512) bheap_fix_kernel(const KArgs a) {
       }
     }
     if (tile_nan)
-      bheap_fix_stage<KMAX, B16, true, NG>(a, cnt, t0, acc, lane_off);
+      bheap_fix_stage<KMAX, B16, true, NG>(a, cnt, t0, acc, lane_off, top);
     else
-      bheap_fix_stage<KMAX, B16, false, NG>(a, cnt, t0, acc, lane_off);
+      bheap_fix_stage<KMAX, B16, false, NG>(a, cnt, t0, acc, lane_off, top);
   }
   if (!live) return;
   finish_row<float, KMAX>(acc, a, row);
