@@ -59,10 +59,60 @@ HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md)
 SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 2.0   # MI355X_MICROARCH.md: wave64 over 2 cycles
 VALU_PEAK = SIMDS * CLOCK_HZ / VALU_CYCLES     # wave64 VALU instructions / s (1,228.8 G)
 VALU_RATE_JSONL = os.path.join(ROOT, "profiles", "r3_valu_rate.jsonl")
-# the binned-heap walk's step (ti_forest_info.walk) -> its row in VALU_RATE_JSONL
-WALK_STEPS = {0: "step r2", 1: "step fixed (and_or, and, cmp_sdwa, cndmask)"}
+# the binned-heap walk (ti_forest_info.walk) -> its step's row in VALU_RATE_JSONL
+# (level 0 from the scalar-loaded root, walk 2, leaves the step itself unchanged)
+WALK_STEPS = {0: "step r2", 1: "step fixed (and_or, and, cmp_sdwa, cndmask)",
+              2: "step fixed (and_or, and, cmp_sdwa, cndmask)"}
 LAYOUT_NAMES = {0: "heap", 1: "explicit", 3: "bheap", 6: "rexplicit", 7: "lexplicit",
                 8: "hexplicit", 9: "texplicit"}
+# the kernel a layout launches (its name in rocprofv3's kernel trace and in the
+# committed PMC passes' "kernel"): a pass describes a launch only if they agree
+LAYOUT_KERNELS = {0: "heap_predict_kernel", 1: "explicit_predict_kernel",
+                  6: "rexplicit_predict_kernel", 7: "lexplicit_predict_kernel",
+                  8: "hexplicit_predict_kernel"}
+WALK_KERNELS = {0: "bheap_predict_kernel", 1: "bheap_fix_kernel", 2: "bheap_fix_kernel"}
+# the committed PMC pass each workload's roofline is priced on
+# (scripts/kernel_pmc.sh -> scripts/make_pmc_json.py)
+PMC_PASSES = {"c2": "profiles/pmc_c2.json", "c3": "profiles/r3_c3_pmc.json",
+              "c3_f64": "profiles/r3_c3_f64_pmc.json", "c3_maxbin": "profiles/r3_c3_maxbin_pmc.json",
+              "c4": "profiles/r3_c4_pmc.json"}
+
+
+def pmc_path(key: str) -> str:
+    return os.path.join(ROOT, PMC_PASSES[key])
+
+
+def launched_kernel(info: dict) -> str:
+    """The predict kernel the engine launches for a forest (ti_forest_info)."""
+    layout = info.get("layout")
+    if layout == 3:
+        return WALK_KERNELS.get(info.get("walk"), "bheap_predict_kernel")
+    if layout == 9:
+        return "t8explicit_predict_kernel" if info.get("bottom") == 1 else "texplicit_predict_kernel"
+    return LAYOUT_KERNELS.get(layout, f"layout{layout}")
+
+
+def pmc_mismatch(pmc, workload: str, rows: int, info: dict):
+    """Why a committed PMC pass does not describe this launch (None: it does).
+    The identity is the workload, the row count, the layout, the launched
+    kernel's name and, for the binned-heap walk, the integer walk id."""
+    if pmc is None:
+        return "no PMC pass file"
+    layout = LAYOUT_NAMES.get(info.get("layout"))
+    want = launched_kernel(info)
+    if pmc.get("workload") != workload:
+        return f"PMC pass is of workload {pmc.get('workload')!r}, not {workload!r}"
+    if pmc.get("layout") != layout:
+        return f"PMC pass is of layout {pmc.get('layout')!r}, this launch is {layout!r}"
+    if f"::{want}<" not in str(pmc.get("kernel", "")):
+        return f"PMC pass kernel {pmc.get('kernel')!r} is not the launched {want}"
+    if info.get("layout") == 3 and pmc.get("walk_id") != info.get("walk"):
+        return f"PMC pass walk id {pmc.get('walk_id')} != the launched walk {info.get('walk')}"
+    if rows is not None and pmc.get("rows") != rows:
+        return f"PMC pass rows {pmc.get('rows')} != {rows}"
+    if "valu_insts_per_launch" not in pmc:
+        return "PMC pass lacks SQ_INSTS_VALU"
+    return None
 
 
 def parse_args(argv=None):
@@ -85,12 +135,18 @@ def parse_args(argv=None):
     p.add_argument("--rows3", type=int, default=100_000_000)
     p.add_argument("--rows4", type=int, default=10_000_000)
     p.add_argument("--config-steps", type=int, default=2)
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, PMC_PASSES["c2"]))
     p.add_argument("--x-buffers", type=int, default=3,
                    help="copies of the batch the timed steps rotate through (3 x 112 MB "
                         "exceeds the 256 MB Infinity Cache)")
     p.add_argument("--host-rows", type=int, default=8_000_000,
                    help="rows of the host-to-host (PCIe-inclusive) C2 leg (0 = skip)")
+    p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
+                   help="cpu: the rank logic only, over gloo, with --engine's stand-in "
+                        "(tests/test_bench_ranks.py)")
+    p.add_argument("--engine", default="",
+                   help="MODULE:FACTORY returning the engine for (forest, local_rank) "
+                        "('' = kfserving_amd.engine.DeviceForest on the rank's GPU)")
     return p.parse_args(argv)
 
 
@@ -192,7 +248,7 @@ def load_pmc(path: str):
         return None
 
 
-def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str, step_op: str = None):
+def roofline(kernel_ms: float, rows: int, info: dict, pmc_path: str):
     """Roofline of the C2 kernel (see the module docstring): the busiest of
     the issue resources the committed PMC pass of the same kernel counts --
     VALU issue, the LDS array, the TD -- each priced on that pass's own
@@ -200,24 +256,28 @@ def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str, step_op: s
     busiest; `achieved` / `peak` are in that resource's unit (LDS-array and TD
     cycles per second per CU against the 2.4 GHz clock; VALU wave64
     instructions per second against the 2-cycle issue peak).  The VALU view,
-    the step-mix ceiling and the HBM view stay beside it."""
+    the step-mix ceiling and the HBM view stay beside it.  A pass that does
+    not describe this launch (pmc_mismatch) leaves `frac` unset and says why
+    in `error`: the line never carries bare nulls."""
+    layout = LAYOUT_NAMES.get(info.get("layout"))
+    step_op = WALK_STEPS.get(info.get("walk")) if info.get("layout") == 3 else None
     pmc = load_pmc(pmc_path)
-    if pmc and not (pmc.get("rows") == rows and pmc.get("workload") == "c2"
-                    and pmc.get("layout") == layout and "valu_insts_per_launch" in pmc
-                    and (step_op is None or pmc.get("walk_step") == step_op)):
-        pmc = None       # a pass of another kernel / size does not describe this one
+    why = pmc_mismatch(pmc, "c2", rows, info)
     t = kernel_ms * 1e-3
     compulsory = (4 * N_FEAT + 4) * rows
     out = {"bound": "valu_issue", "unit": "Ginst/s", "peak": VALU_PEAK / 1e9,
-           "achieved": None, "frac": None, "traffic": None, "kernel_ms": kernel_ms,
+           "kernel": launched_kernel(info), "kernel_ms": kernel_ms,
            "peak_basis": f"{SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz / {VALU_CYCLES:g} cycles per "
                          "wave64 VALU instruction (MI355X_MICROARCH.md)",
            "hbm_compulsory_bytes": compulsory,
+           "hbm_compulsory_GBps": compulsory / t / 1e9,
            "hbm_compulsory_frac": compulsory / t / HBM_PEAK}
-    if not pmc:
+    if why:
+        out.update(achieved=None, frac=None, traffic=None,
+                   error=f"{os.path.relpath(pmc_path, ROOT)}: {why}")
         return out
     valu = pmc["valu_insts_per_launch"]
-    cfg = config_roofline(kernel_ms, rows, layout, "c2", pmc_path) or {}
+    cfg = config_roofline(kernel_ms, rows, info, "c2", pmc_path) or {}
     fr = cfg.get("fracs") or {}
     valu_view = {"achieved": valu / t / 1e9, "peak": VALU_PEAK / 1e9, "unit": "Ginst/s",
                  "frac": valu / t / VALU_PEAK, "valu_insts_per_launch": valu,
@@ -259,16 +319,18 @@ def roofline(kernel_ms: float, rows: int, layout: str, pmc_path: str, step_op: s
             out[k] = pmc[k]
     out["traffic"] = pmc.get("hbm_bytes_per_launch")
     if out["traffic"]:
+        out["hbm_counter_GBps"] = out["traffic"] / t / 1e9
         out["hbm_counter_frac"] = out["traffic"] / t / HBM_PEAK
         out["traffic_over_compulsory"] = out["traffic"] / (compulsory + pmc.get("model_bytes", 0))
     out["pmc_source"] = pmc.get("source")
+    out["pmc_kernel"] = pmc.get("kernel")
     return out
 
 
 CUS = 256
 
 
-def config_roofline(kernel_ms: float, rows: int, layout: str, workload: str, pmc_path: str):
+def config_roofline(kernel_ms: float, rows: int, info: dict, workload: str, pmc_path: str):
     """Binding-resource roofline of a C3 / C4 launch from a committed PMC pass
     of the same kernel at 1M rows (scripts/kernel_pmc.sh ->
     scripts/make_pmc_json.py).  Three issue-type resources are priced, each
@@ -280,8 +342,9 @@ def config_roofline(kernel_ms: float, rows: int, layout: str, workload: str, pmc
     run's time; `fracs_bench` re-prices the per-row counts on this run's
     kernel time at the nominal 2.4 GHz.  `bound` is the busiest resource."""
     pmc = load_pmc(pmc_path)
-    if not pmc or pmc.get("workload") != workload or pmc.get("layout") != layout:
-        return None       # a pass of another kernel does not describe this one
+    why = pmc_mismatch(pmc, workload, None, info)
+    if why:               # a pass of another kernel does not describe this one
+        return {"bound": None, "frac": None, "error": f"{os.path.relpath(pmc_path, ROOT)}: {why}"}
     cyc = pmc.get("gui_active_cycles_per_xcd")
     # (count, units, the cycles of the pass that counted it)
     counts = {"valu_issue": (pmc["valu_insts_per_launch"] * VALU_CYCLES, SIMDS,
@@ -513,7 +576,7 @@ def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_
                "compulsory_GBps": ((X.element_size() * n_feat + out.element_size()) * rows
                                    / (kms * 1e-3) / 1e9 if kms else None)}
         if pmc_path and kms:
-            res["roofline"] = config_roofline(kms, rows, res["layout"], pmc_workload, pmc_path)
+            res["roofline"] = config_roofline(kms, rows, eng.info(), pmc_workload, pmc_path)
         if cpu_fn is not None and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_fn(lambda n: X[:min(rows, n)].cpu().numpy())
     del X, out
@@ -697,7 +760,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             dt = "float64" if name == "c3_f64" else "float32"
             r = run_config(f3, 100, args.rows3, 3, args, world, rank, device, dev_sync,
                            make_engine, c3_cpu(t3, args.cpu_seconds / 2, dt), name,
-                           os.path.join(ROOT, "profiles", f"r3_{name}_pmc.json"), dt)
+                           pmc_path(name), dt)
             if r is not None:
                 r.update(config=f"C3 LightGBM leaf-wise 1000 trees x 255 leaves, 100 features, "
                                 f"{dt} input, float64 sigmoid of the raw score", model=src)
@@ -705,7 +768,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             f4, raw4, src = c4_forest()
             r = run_config(f4, 64, args.rows4, 2, args, world, rank, device, dev_sync,
                            make_engine, c4_cpu(raw4, args.cpu_seconds / 2), "c4",
-                           os.path.join(ROOT, "profiles", "r3_c4_pmc.json"))
+                           pmc_path("c4"))
             if r is not None:
                 cb = r.pop("cpu_baseline", None)
                 if cb:
@@ -740,8 +803,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
                        "rows_per_gpu": rows, "trees": N_TREES, "depth": DEPTH,
                        "features": N_FEAT, "layout": LAYOUT_NAMES.get(info["layout"]),
                        "parallelism": f"rows sharded x{world}", "x_buffers": len(Xs)},
-            "roofline": roofline(kernel_ms, rows, LAYOUT_NAMES.get(info["layout"]),
-                                 args.pmc_json, WALK_STEPS.get(info.get("walk"))),
+            "roofline": roofline(kernel_ms, rows, info, args.pmc_json),
             "cpu_baseline": cpu,
             "batched_latency": latency,
             "nan_variant": nan_variant,
@@ -754,8 +816,50 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
     return line
 
 
-def main():
-    line = run(parse_args())
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` started without a launcher: start N ranks, one
+    process per GPU, under torch.distributed.run (a child process, never an
+    exec: nothing here has touched the GPU) and return its exit code.  Rank 0
+    prints the JSON line; value = all ranks' rows / the slowest rank's wall
+    (the reference's parallelism this stands for: KFServer's pre-forked
+    workers, python/kfserving/kfserving/kfserver.py:99)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, host_threads() // n)))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def resolve_engine(spec: str):
+    """--engine MODULE:FACTORY -> make_engine(forest) for this rank (None: the GPU engine)."""
+    if not spec:
+        return None
+    import importlib
+    mod, _, attr = spec.partition(":")
+    factory = getattr(importlib.import_module(mod), attr)
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    return lambda forest: factory(forest, local_rank)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, argv))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; timing {world} rank(s)",
+              file=sys.stderr, flush=True)
+    backend = "gloo" if args.device == "cpu" else "nccl"
+    line = run(args, device=args.device, backend=backend, make_engine=resolve_engine(args.engine))
     if line is not None:
         print(json.dumps(line), flush=True)
 

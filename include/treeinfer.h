@@ -164,7 +164,8 @@ typedef struct ti_forest_info {
   int64_t device_bytes;       /* forest bytes resident per device                   */
   int64_t tree_stride_bytes;  /* heap layout: bytes per staged tree                 */
   int32_t walk;               /* binned heap walk of float32 input: 0 indexed step
-                                 (5 VALU), 1 fixed-layout step (4 VALU)  */
+                                 (5 VALU), 1 fixed-layout step (4 VALU),
+                                 2 fixed-layout step with the scalar-loaded root     */
   int32_t bin_bits;           /* 8 or 16: bin width of the float32 image (0: none)   */
   int32_t tree_ilp;           /* record layouts: trees walked at once per lane       */
   int32_t n_stages;           /* staged layouts (7, 9): LDS stages of the forest     */

@@ -3103,7 +3103,8 @@ int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
     for (auto& p : f->parts) info->device_bytes += p->devs.empty() ? 0 : p->devs[0]->bytes;
   }
   info->tree_stride_bytes = f->layout == 0 ? f->stride32 : f->layout == 3 ? f->bh[0].stride : 0;
-  info->walk = bheap_fixed(f, TI_F32, TI_OUTPUT_PREDICT) ? 1 : 0;
+  // walk id: the kernel variant a PMC pass was taken on (bench.py matches it)
+  info->walk = bheap_fixed(f, TI_F32, TI_OUTPUT_PREDICT) ? (TI_FIX_SROOT ? 2 : 1) : 0;
   info->bin_bits = f->layout == 3 ? (f->bh[0].b16 ? 16 : 8)
                    : (f->layout >= 6 && f->layout <= 9) ? (f->rx[0].b8 ? 8 : 16) : 0;
   info->tree_ilp = f->layout == 6 ? f->rx_ilp : f->layout == 8 ? f->hx_ilp

@@ -13,7 +13,10 @@ kernel) into the per-launch figures bench.py prices its rooflines with
     "DVFS give-back").
 
 Usage: python scripts/make_pmc_json.py PROF_DIR KERNEL_SUBSTR WORKLOAD LAYOUT ROWS OUT.json
-           [--walk-step NAME] [--model-bytes N] [--source TEXT]
+           [--walk-step NAME] [--walk-id N] [--model-bytes N] [--source TEXT]
+
+--walk-id is ti_forest_info.walk of the profiled binned-heap launch: bench.py
+matches it (and the kernel name) against the launch it prices.
 """
 import argparse
 import csv
@@ -57,6 +60,7 @@ def main():
     p.add_argument("rows", type=int)
     p.add_argument("out")
     p.add_argument("--walk-step", default=None)
+    p.add_argument("--walk-id", type=int, default=None)
     p.add_argument("--model-bytes", type=int, default=0)
     p.add_argument("--source", default=None)
     a = p.parse_args()
@@ -76,7 +80,7 @@ def main():
 
     res = {"workload": a.workload, "layout": a.layout, "rows": a.rows,
            "kernel": meta.get("Kernel_Name"), "vgprs": meta.get("VGPR_Count"),
-           "sgprs": meta.get("SGPR_Count"), "walk_step": a.walk_step,
+           "sgprs": meta.get("SGPR_Count"), "walk_step": a.walk_step, "walk_id": a.walk_id,
            "model_bytes": a.model_bytes,
            "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
            "waves_per_launch": c.get("SQ_WAVES"),

@@ -1,11 +1,16 @@
 """bench.py's rank path end to end on CPU (gloo, world size 2) with a stub
 engine: weak-scaling headline (every rank its own batch), max-over-ranks wall
 time, strong-scaling C3 shard, and the JSON line rank 0 assembles."""
+import json
 import os
 import socket
+import subprocess
+import sys
 import time
 
 import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -82,3 +87,25 @@ def test_bench_rank_path_two_ranks():
     rf = line["roofline"]
     assert rf["bound"] == "valu_issue" and rf["unit"] == "Ginst/s"
     assert 0 < rf["hbm_compulsory_frac"] < 1
+
+
+def test_bench_cli_gpus_n_starts_n_ranks():
+    """`python bench.py --gpus 2` as the driver runs it (no launcher, no
+    WORLD_SIZE): bench.py starts the two ranks itself, only rank 0 prints,
+    n_gpus is 2 and value = both ranks' rows / the slowest rank's wall."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--engine", "tests.bench_stub:make", "--steps", "5", "--warmup", "1",
+           "--rows", "2048", "--configs", "", "--no-cpu-baseline", "--latency-qps", "0",
+           "--nan-variant", "0", "--host-rows", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout                      # rank 0 alone prints
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["parallelism"] == "rows sharded x2"
+    assert line["ms_per_step"] >= 20.0                    # rank 1's 20 ms steps dominate
+    want = 2048 * 2 * 5 / (line["ms_per_step"] * 5e-3)
+    assert abs(line["value"] - want) < 1e-6 * want

@@ -1,0 +1,37 @@
+"""On the GPU: the kernels the engine picks for the bench's forests are the
+ones the committed PMC passes were taken on (bench.pmc_mismatch), so the
+driver's bench line carries a roofline and not an `error`."""
+import os
+
+import pytest
+
+import bench
+
+pytestmark = pytest.mark.gpu
+
+
+def _info(forest):
+    from kfserving_amd.engine import DeviceForest
+    dev = DeviceForest(forest, devices=[0])
+    try:
+        return dev.info()
+    finally:
+        dev.close()
+
+
+def test_c2_launch_matches_pmc_pass():
+    _, _, forest = bench.build_model()
+    info = _info(forest)
+    pmc = bench.load_pmc(bench.pmc_path("c2"))
+    assert bench.pmc_mismatch(pmc, "c2", bench.ROWS, info) is None, info
+    rf = bench.roofline(0.72, bench.ROWS, info, bench.pmc_path("c2"))
+    assert rf["frac"] and rf["traffic"] and rf["lds_bank_conflict_frac"] is not None
+
+
+@pytest.mark.parametrize("key", ["c3", "c3_maxbin", "c4"])
+def test_config_launch_matches_pmc_pass(key):
+    forest = {"c3": bench.c3_forest, "c3_maxbin": bench.c3_maxbin_forest,
+              "c4": bench.c4_forest}[key]()[0]
+    info = _info(forest)
+    pmc = bench.load_pmc(bench.pmc_path(key))
+    assert bench.pmc_mismatch(pmc, key, None, info) is None, info
