@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define TI_ABI_VERSION 3
+#define TI_ABI_VERSION 4
 
 /* return codes */
 #define TI_OK               0
@@ -171,7 +171,23 @@ typedef struct ti_forest_info {
   int32_t n_stages;           /* staged layouts (7, 9): LDS stages of the forest     */
   int32_t top_depth;          /* layouts 8, 9: levels of each tree's heap top        */
   int32_t bottom;             /* layout 9: 0 records, 1 compact u8 nodes (plan_tx8)  */
+  /* ABI 4: the TreeSHAP coefficient table of device slot 0 */
+  int32_t shap_table;         /* 1 built, 0 not (yet) built, -1 not buildable: over
+                                 TI_OPT_SHAP_TABLE_MB or its allocation failed; the
+                                 extend / unwind kernel serves every batch          */
+  int32_t reserved1;
+  int64_t shap_table_bytes;   /* device bytes of the built table                     */
+  double  shap_table_build_ms;/* host wall time of the last table build             */
 } ti_forest_info;
+
+/* ti_forest_set_option options (ABI 4) */
+#define TI_OPT_SHAP_TABLE_ROWS 1  /* TI_OUTPUT_CONTRIB batches of at most this many rows
+                                     use the TreeSHAP coefficient table (0: never);
+                                     default 16384 or $TI_SHAP_TABLE_ROWS            */
+#define TI_OPT_SHAP_TABLE_MB   2  /* build the table only if it fits this many MiB per
+                                     device (0: never); default 1280 or
+                                     $TI_SHAP_TABLE_MB; read when a replica's table
+                                     is first needed                                */
 
 /* Upload the forest to each listed device (HIP device ordinals).  HIP is
  * initialised here, not at library load, so a process may fork before it.
@@ -185,6 +201,13 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices,
 int ti_forest_destroy(ti_forest* forest);
 
 int ti_forest_get_info(const ti_forest* forest, ti_forest_info* info);
+
+/* Per-forest tuning that changes speed, never results (both TreeSHAP kernels
+ * produce the same contributions).  0 or TI_ERR_INVALID for an unknown option
+ * or a negative value.  Replaces nothing in the libraries: xgboost and
+ * LightGBM have no TreeSHAP table; this is the engine's own knob (the
+ * :explain route, python/kfserving/kfserving/kfserver.py:79-82). */
+int ti_forest_set_option(ti_forest* forest, int32_t option, int64_t value);
 
 /* Number of elements and element type ti_predict writes for n_rows rows. */
 int ti_output_shape(const ti_forest* forest, int32_t output_kind, int64_t n_rows,

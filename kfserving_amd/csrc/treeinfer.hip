@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cmath>
 #include <limits>
@@ -454,6 +455,11 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+int fail_hip(hipError_t e, const char* what) {
+  if (e == hipSuccess) return TI_OK;
+  return fail(TI_ERR_DEVICE, std::string(what) + " failed: " + hipGetErrorString(e));
+}
+
 #define TI_HIP(expr)                                                                    \
   do {                                                                                  \
     hipError_t e_ = (expr);                                                             \
@@ -542,6 +548,8 @@ struct DeviceForest {
   double* shap_bias = nullptr;
   void* shap_tab = nullptr;          // TreeSHAP coefficient table (shap_table_kernel), MT-typed
   int64_t* shap_tab_off = nullptr;   // [paths] first coefficient of each path
+  int32_t shap_tab_state = 0;        // 0 not tried, 1 built, -1 failed or over the cap:
+                                     // contributions use the extend / unwind kernel
   // ti_predict scratch: device buffers + pinned host staging (grown x2)
   void* x_buf = nullptr;
   size_t x_cap = 0;
@@ -644,10 +652,18 @@ struct ti_forest {
   std::unique_ptr<ShapSource> shap_src;
   std::vector<ShapPath> h_paths;
   // TreeSHAP coefficient table: per path, (2^n one-patterns) x n coefficients
-  // (contrib_reg_kernel TAB); shap_tab_mt = 4 / 8 bytes per coefficient, 0: none
+  // (contrib_reg_kernel TAB); shap_tab_mt = 4 / 8 bytes per coefficient, 0: the
+  // forest's paths cannot use one.  Built per replica on the first
+  // contributions batch of at most shap_tab_rows rows, if its bytes stay under
+  // shap_tab_mb (ti_forest_set_option; defaults $TI_SHAP_TABLE_ROWS /
+  // $TI_SHAP_TABLE_MB read at ti_forest_create); optional: a failed build
+  // leaves the extend / unwind kernel in charge.
   int32_t shap_tab_mt = 0;
   std::vector<int64_t> h_tab_off;
   int64_t shap_tab_len = 0;
+  int64_t shap_tab_rows = env_int("TI_SHAP_TABLE_ROWS", 16384);
+  int64_t shap_tab_mb = env_int("TI_SHAP_TABLE_MB", 1280);
+  double shap_tab_build_ms = 0.0;   // the last table build (slot's shap_table_kernel + upload)
   std::vector<ShapElem> h_elems;
   std::vector<double> h_path_leaf, h_shap_bias;
   // host images (kept until upload)
@@ -727,6 +743,19 @@ void free_device(DeviceForest& d) {
   d.x_cap = d.out_cap = 0;
   d.stream = nullptr;
   d.device = -1;
+}
+
+// the TreeSHAP buffers of one replica (device current), after a failed upload
+void free_shap(DeviceForest& d) {
+  void* ptrs[] = {d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias, d.shap_tab, d.shap_tab_off};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  d.shap_paths = nullptr;
+  d.shap_elems = nullptr;
+  d.shap_leaf = d.shap_bias = nullptr;
+  d.shap_tab = nullptr;
+  d.shap_tab_off = nullptr;
+  d.shap_tab_state = 0;
 }
 
 // -------------------------------------------------------------- validation
@@ -2567,62 +2596,102 @@ int ensure_shap(ti_forest* f) {
   if (f->shap_ready.load(std::memory_order_acquire)) return TI_OK;
   std::lock_guard<std::mutex> lk(f->shap_mu);
   if (f->shap_ready.load(std::memory_order_relaxed)) return TI_OK;
-  build_shap(&f->shap_src->desc, f);
-  // the coefficient table (contrib_reg_kernel TAB): paths of <= 8 unique
-  // features, 2^n x 8 coefficients each (padded), in the path arithmetic's type;
-  // built when the whole table stays under TI_SHAP_TABLE_MB (2048; 0: never)
+  if (f->h_paths.empty()) build_shap(&f->shap_src->desc, f);
+  // the coefficient table's shape (contrib_reg_kernel TAB): paths of <= 8
+  // unique features, 2^n x 8 coefficients each (padded), in the path
+  // arithmetic's type.  The table itself is built per replica, later, by
+  // ensure_shap_table.
   {
-    static const int table_mb = env_int("TI_SHAP_TABLE_MB", 2048);
-    static const int force_f64 = env_int("TI_SHAP_F64", 0);
-    const int mt = (f->accum != TI_F64 && !force_f64) ? 4 : 8;
+    const int mt = (f->accum != TI_F64 && !env_int("TI_SHAP_F64", 0)) ? 4 : 8;
     const int64_t W = static_cast<int64_t>(f->K) * (f->F + 1);
     f->h_tab_off.assign(f->h_paths.size(), 0);
     int64_t len = 0;
-    bool ok = table_mb > 0 && W <= kShapLdsW && f->shap_maxl <= kShapTabStride;
+    bool ok = W <= kShapLdsW && f->shap_maxl <= kShapTabStride && !f->h_paths.empty();
     for (size_t i = 0; ok && i < f->h_paths.size(); ++i) {
       f->h_tab_off[i] = len;
       len += (int64_t(1) << f->h_paths[i].n) * kShapTabStride;
-      ok = len * mt <= static_cast<int64_t>(table_mb) << 20;
     }
-    f->shap_tab_mt = ok && !f->h_paths.empty() ? mt : 0;
-    f->shap_tab_len = f->shap_tab_mt ? len : 0;
-    if (!f->shap_tab_mt) f->h_tab_off.clear();
+    f->shap_tab_mt = ok ? mt : 0;
+    f->shap_tab_len = ok ? len : 0;
+    if (!ok) f->h_tab_off.clear();
   }
   int dev0 = 0;
   TI_HIP(hipGetDevice(&dev0));
   int rc = TI_OK;
   for (auto& dp : f->devs) {
     DeviceForest& d = *dp;
-    TI_HIP(hipSetDevice(d.device));
+    if ((rc = fail_hip(hipSetDevice(d.device), "hipSetDevice"))) break;
     if ((rc = upload(&d.shap_paths, f->h_paths, &d.bytes)) ||
         (rc = upload(&d.shap_elems, f->h_elems, &d.bytes)) ||
         (rc = upload(&d.shap_leaf, f->h_path_leaf, &d.bytes)) ||
         (rc = upload(&d.shap_bias, f->h_shap_bias, &d.bytes)))
       break;
-    if (f->shap_tab_mt) {
-      if ((rc = upload(&d.shap_tab_off, f->h_tab_off, &d.bytes))) break;
-      const size_t bytes = static_cast<size_t>(f->shap_tab_len) * f->shap_tab_mt;
-      TI_HIP(hipMalloc(&d.shap_tab, std::max<size_t>(bytes, 16)));
-      d.bytes += static_cast<int64_t>(bytes);
-      const unsigned np = static_cast<unsigned>(f->h_paths.size());
-      if (f->shap_tab_mt == 4)
-        hipLaunchKernelGGL((shap_table_kernel<float, 16>), dim3(np), dim3(256), 0, nullptr,
-                           d.shap_paths, d.shap_elems, d.shap_tab_off, static_cast<float*>(d.shap_tab));
-      else
-        hipLaunchKernelGGL((shap_table_kernel<double, 16>), dim3(np), dim3(256), 0, nullptr,
-                           d.shap_paths, d.shap_elems, d.shap_tab_off, static_cast<double*>(d.shap_tab));
-      TI_HIP(hipGetLastError());
-      TI_HIP(hipDeviceSynchronize());
+  }
+  if (rc) {
+    // nothing half-built survives: every replica's path tables are freed (the
+    // host tables stay, so the next call retries from them)
+    const std::string err = g_last_error;
+    for (auto& dp : f->devs) {
+      (void)hipSetDevice(dp->device);
+      free_shap(*dp);
     }
+    (void)hipGetLastError();
+    (void)hipSetDevice(dev0);
+    return fail(rc, err);
   }
   TI_HIP(hipSetDevice(dev0));
-  if (rc) return rc;
   f->h_paths.clear(); f->h_paths.shrink_to_fit();
   f->h_elems.clear(); f->h_elems.shrink_to_fit();
   f->h_path_leaf.clear(); f->h_path_leaf.shrink_to_fit();
   f->shap_src.reset();
   f->shap_ready.store(true, std::memory_order_release);
   return TI_OK;
+}
+
+// The coefficient table of one replica (device d.device current), built on
+// the first contributions batch that would use it.  It is an optimisation
+// only: any failure (over the size cap, allocation, launch) frees what was
+// allocated, clears the HIP error and marks the replica, whose contributions
+// then take the extend / unwind kernel -- never an error for the caller.  The
+// build runs on a private stream and waits for that stream alone.
+void ensure_shap_table(ti_forest* f, DeviceForest& d) {
+  std::lock_guard<std::mutex> lk(f->shap_mu);
+  if (d.shap_tab_state != 0) return;
+  d.shap_tab_state = -1;
+  const size_t bytes = static_cast<size_t>(f->shap_tab_len) * f->shap_tab_mt;
+  if (!f->shap_tab_mt || f->shap_tab_mb <= 0 ||
+      bytes > (static_cast<size_t>(f->shap_tab_mb) << 20))
+    return;
+  const auto t0 = std::chrono::steady_clock::now();
+  hipStream_t s = nullptr;
+  bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+  int64_t up = 0;
+  ok = ok && !env_int("TI_SHAP_TABLE_FAULT", 0) &&   // fault injection (tests)
+       upload(&d.shap_tab_off, f->h_tab_off, &up) == TI_OK &&
+       hipMalloc(&d.shap_tab, std::max<size_t>(bytes, 16)) == hipSuccess;
+  if (ok) {
+    const unsigned np = static_cast<unsigned>(f->h_tab_off.size());
+    if (f->shap_tab_mt == 4)
+      hipLaunchKernelGGL((shap_table_kernel<float, 16>), dim3(np), dim3(256), 0, s,
+                         d.shap_paths, d.shap_elems, d.shap_tab_off, static_cast<float*>(d.shap_tab));
+    else
+      hipLaunchKernelGGL((shap_table_kernel<double, 16>), dim3(np), dim3(256), 0, s,
+                         d.shap_paths, d.shap_elems, d.shap_tab_off, static_cast<double*>(d.shap_tab));
+    ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+  }
+  if (s) (void)hipStreamDestroy(s);
+  if (!ok) {
+    if (d.shap_tab) (void)hipFree(d.shap_tab);
+    if (d.shap_tab_off) (void)hipFree(d.shap_tab_off);
+    d.shap_tab = nullptr;
+    d.shap_tab_off = nullptr;
+    (void)hipGetLastError();
+    return;
+  }
+  d.bytes += up + static_cast<int64_t>(bytes);
+  d.shap_tab_state = 1;
+  f->shap_tab_build_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows,
@@ -2636,11 +2705,11 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
   }
   const int64_t W = static_cast<int64_t>(f->K) * (f->F + 1);
   const int64_t n_paths = static_cast<int64_t>(d.shap_paths ? 1 : 0) * f->shap_npaths;
-  static const int force_generic = env_int("TI_SHAP_GENERIC", 0);
+  const int force_generic = env_int("TI_SHAP_GENERIC", 0);
   if (W <= kShapLdsW && f->shap_maxl <= 32 && !force_generic) {
     // registers + LDS accumulators: no scratch accumulator, no memset
     const int maxn = f->shap_maxl <= 8 ? 8 : f->shap_maxl <= 16 ? 16 : 32;
-    static const int force_f64 = env_int("TI_SHAP_F64", 0);
+    const int force_f64 = env_int("TI_SHAP_F64", 0);
     const bool f32_math = f->accum != TI_F64 && !force_f64;
     const size_t lds_w = static_cast<size_t>(W) * 64 * (f32_math ? 4 : 8);
     const unsigned grid_r = static_cast<unsigned>((rows + 63) / 64);
@@ -2648,7 +2717,7 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
     // Path slices: one 64-row wave walks n_paths / slices paths, so a small
     // batch still fills the 256 CUs (>= kShapWaveTarget waves); partials
     // [slices][W][rows] are summed in slice order by contrib_slices_kernel.
-    static const int force_slices = env_int("TI_SHAP_SLICES", 0);
+    const int force_slices = env_int("TI_SHAP_SLICES", 0);
     int64_t slices = force_slices > 0 ? force_slices
                                       : (kShapWaveTarget + grid_r - 1) / static_cast<int64_t>(grid_r);
     slices = std::min<int64_t>(slices, std::max<int64_t>(1, n_paths / kShapMinPathsPerSlice));
@@ -2660,15 +2729,16 @@ int launch_contrib(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_
     // 4.1e5 vs 2.7e5 rows/s); at 100k rows its gathers (a 64-row wave reads
     // most of each path's 2^n x 32 B block) make it slower than the extend /
     // unwind arithmetic (2.2e5 vs 2.9e5): profiles/r3_shap_table.jsonl
-    static const int64_t tab_rows = env_int("TI_SHAP_TABLE_ROWS", 16384);
+    const bool want_tab = f->shap_tab_mt != 0 && rows <= f->shap_tab_rows;
+    if (want_tab && d.shap_tab_state == 0) ensure_shap_table(f, d);
     double* part = nullptr;
     if (slices > 1)
       TI_HIP(hipMallocAsync(reinterpret_cast<void**>(&part),
                             static_cast<size_t>(slices * W * rows) * 8, stream));
 #define TI_CONTRIB_REG(XT_, ACC_, MT_, N_)                                                          \
   do {                                                                                         \
-    const bool tab_ = d.shap_tab != nullptr && f->shap_tab_mt == (int)sizeof(MT_) &&           \
-                      rows <= tab_rows;                                                        \
+    const bool tab_ = want_tab && d.shap_tab_state == 1 &&                                     \
+                      f->shap_tab_mt == (int)sizeof(MT_);                                      \
     KernelFn fn_ = tab_ ? reinterpret_cast<KernelFn>(contrib_reg_kernel<XT_, ACC_, MT_, 8, true>) \
                         : reinterpret_cast<KernelFn>(contrib_reg_kernel<XT_, ACC_, MT_, N_>);  \
     int rc_ = ensure_lds_attr(d.device, fn_);                                                  \
@@ -3113,7 +3183,34 @@ int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
                        ? static_cast<int32_t>(f->h_lx_stage.size() - 1) : 0;
   info->top_depth = (f->layout == 8 || f->layout == 9) ? f->hx_top : 0;
   info->bottom = f->layout == 9 ? f->tx8 : 0;
+  // the TreeSHAP coefficient table of slot 0 (of the first part)
+  const ti_forest* sf = f->parts.empty() ? f : f->parts[0].get();
+  info->shap_table = sf->devs.empty() ? 0 : sf->devs[0]->shap_tab_state;
+  info->reserved1 = 0;
+  info->shap_table_bytes = info->shap_table == 1 ? sf->shap_tab_len * sf->shap_tab_mt : 0;
+  info->shap_table_build_ms = sf->shap_tab_build_ms;
   return TI_OK;
+}
+
+int ti_forest_set_option(ti_forest* f, int32_t option, int64_t value) {
+  if (!f) return fail(TI_ERR_INVALID, "null forest");
+  for (auto& p : f->parts) {
+    const int rc = ti_forest_set_option(p.get(), option, value);
+    if (rc) return rc;
+  }
+  std::lock_guard<std::mutex> lk(f->shap_mu);
+  switch (option) {
+    case TI_OPT_SHAP_TABLE_ROWS:
+      if (value < 0) return fail(TI_ERR_INVALID, "TI_OPT_SHAP_TABLE_ROWS must be >= 0");
+      f->shap_tab_rows = value;
+      return TI_OK;
+    case TI_OPT_SHAP_TABLE_MB:
+      if (value < 0) return fail(TI_ERR_INVALID, "TI_OPT_SHAP_TABLE_MB must be >= 0");
+      f->shap_tab_mb = value;
+      return TI_OK;
+    default:
+      return fail(TI_ERR_INVALID, "unknown option " + std::to_string(option));
+  }
 }
 
 int ti_output_shape(const ti_forest* f, int32_t kind, int64_t n_rows, int64_t* out_len,

@@ -21,15 +21,19 @@ import numpy as np
 from .forest import (Forest, OUT_CONTRIB, OUT_LEAF, OUT_MARGIN, OUT_PREDICT, TI_F32, TI_F64,
                      TI_I32)
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("TREEINFER_LIB", os.path.join(_LIB_DIR, "libtreeinfer.so"))
 
 EXPORTED_SYMBOLS = (
     "ti_forest_create", "ti_forest_destroy", "ti_forest_get_info", "ti_output_shape",
     "ti_predict", "ti_predict_device", "ti_transform_device", "ti_last_error", "ti_device_count",
-    "ti_abi_version",
+    "ti_abi_version", "ti_forest_set_option",
 )
+
+# ti_forest_set_option options (include/treeinfer.h)
+OPT_SHAP_TABLE_ROWS = 1
+OPT_SHAP_TABLE_MB = 2
 
 
 class TreeInferError(RuntimeError):
@@ -89,6 +93,10 @@ class _ForestInfo(ctypes.Structure):
         ("n_stages", ctypes.c_int32),
         ("top_depth", ctypes.c_int32),
         ("bottom", ctypes.c_int32),
+        ("shap_table", ctypes.c_int32),
+        ("reserved1", ctypes.c_int32),
+        ("shap_table_bytes", ctypes.c_int64),
+        ("shap_table_build_ms", ctypes.c_double),
     ]
 
 
@@ -127,6 +135,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.ti_predict.argtypes = [vp, vp, i32, i64, i32, i64, i32, vp, i64]
         lib.ti_predict_device.restype = ctypes.c_int
         lib.ti_predict_device.argtypes = [vp, i32, vp, i32, i64, i32, i64, i32, vp, i64, vp]
+        lib.ti_forest_set_option.restype = ctypes.c_int
+        lib.ti_forest_set_option.argtypes = [vp, i32, i64]
         lib.ti_transform_device.restype = ctypes.c_int
         lib.ti_transform_device.argtypes = [vp, i32, vp, i64, vp, i64, vp]
         if lib.ti_abi_version() != ABI_VERSION:
@@ -216,6 +226,11 @@ class DeviceForest:
         _check(self._lib, self._lib.ti_forest_get_info(self._handle, ctypes.byref(inf)))
         return {k: getattr(inf, k) for k, _ in _ForestInfo._fields_}
 
+    def set_option(self, option: int, value: int) -> None:
+        """ti_forest_set_option: speed knobs that never change results
+        (OPT_SHAP_TABLE_ROWS, OPT_SHAP_TABLE_MB)."""
+        _check(self._lib, self._lib.ti_forest_set_option(self._handle, option, int(value)))
+
     def output_shape(self, kind: int, n_rows: int):
         n = ctypes.c_int64()
         dt = ctypes.c_int32()
@@ -280,5 +295,6 @@ class DeviceForest:
 
 
 __all__ = ["DeviceForest", "TreeInferError", "load_library", "device_count", "default_devices",
+           "OPT_SHAP_TABLE_ROWS", "OPT_SHAP_TABLE_MB",
            "EXPORTED_SYMBOLS", "OUT_MARGIN", "OUT_PREDICT", "OUT_LEAF", "OUT_CONTRIB", "TI_F32", "TI_F64",
            "TI_I32"]

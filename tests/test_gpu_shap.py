@@ -13,7 +13,8 @@ import tempfile
 import numpy as np
 import pytest
 
-from kfserving_amd.engine import DeviceForest, TreeInferError
+from kfserving_amd.engine import (OPT_SHAP_TABLE_MB, OPT_SHAP_TABLE_ROWS, DeviceForest,
+                                  TreeInferError)
 from kfserving_amd.forest import OUT_CONTRIB, OUT_MARGIN, TI_F32
 from kfserving_amd.formats import load_lightgbm_model, load_xgboost_model
 from kfserving_amd.formats import lightgbm_format as lf
@@ -84,11 +85,71 @@ def _check(f, X, got):
     (lambda: _sk("gb-reg"), False),
 ], ids=["xgb", "xgb-multiclass", "lgb-zero-missing", "lgb-multiclass", "sk-rf-clf",
         "sk-rf-reg", "sk-gb-reg"])
-def test_contributions_match_oracle(make, nan):
+@pytest.mark.parametrize("kernel", ["table", "arith"])
+def test_contributions_match_oracle(make, nan, kernel):
+    """Both TreeSHAP kernels against the oracle: the coefficient table (small
+    batches) and the extend / unwind arithmetic (batches over
+    TI_OPT_SHAP_TABLE_ROWS), forced per forest."""
     f = make()
     X = _rows(f, 130, seed=11, nan=nan)        # 130 rows: two full 64-row blocks + a ragged one
-    got = DeviceForest(f, [0]).predict(X, OUT_CONTRIB)
+    dev = DeviceForest(f, [0])
+    dev.set_option(OPT_SHAP_TABLE_ROWS, 1 << 30 if kernel == "table" else 0)
+    got = dev.predict(X, OUT_CONTRIB)
     _check(f, X, got)
+    info = dev.info()
+    if kernel == "arith":
+        assert info["shap_table"] == 0          # never needed, never built
+    elif f.accum_dtype == TI_F32:               # xgboost: paths of <= 8 features
+        assert info["shap_table"] == 1 and info["shap_table_bytes"] > 0
+
+
+def test_table_and_arithmetic_bit_identical_c2_shape():
+    """The C2-shape forest (500 x depth 8, 28 features) at 4,096 rows: the
+    table kernel's contributions are the arithmetic kernel's, bit for bit (the
+    table holds the same float32 expressions in the same order)."""
+    f = _xgb(500, 8, 28, seed=21)
+    X = _rows(f, 4096, seed=22)
+    dev = DeviceForest(f, [0])
+    tab = dev.predict(X, OUT_CONTRIB)
+    info = dev.info()
+    assert info["shap_table"] == 1, info
+    assert info["shap_table_build_ms"] > 0
+    print(f"C2-shape table: {info['shap_table_bytes'] / 2**20:.0f} MiB built in "
+          f"{info['shap_table_build_ms']:.0f} ms")
+    dev.set_option(OPT_SHAP_TABLE_ROWS, 0)
+    arith = dev.predict(X, OUT_CONTRIB)
+    assert np.array_equal(tab, arith)
+    _check(f, X[:200], tab[:200])
+
+
+@pytest.mark.parametrize("how", ["fault", "cap0", "cap_small"])
+def test_table_failure_falls_back_to_arithmetic(how, monkeypatch):
+    """The table is optional: an allocation/launch failure (injected) or a size
+    cap it exceeds leaves the extend / unwind kernel serving the batch, with
+    the same contributions, and no error for the caller."""
+    f = _xgb(40, 6, 12, seed=23)
+    X = _rows(f, 300, seed=24)
+    ref = DeviceForest(f, [0])
+    ref.set_option(OPT_SHAP_TABLE_ROWS, 0)
+    want = ref.predict(X, OUT_CONTRIB)
+    dev = DeviceForest(f, [0])
+    if how == "fault":
+        monkeypatch.setenv("TI_SHAP_TABLE_FAULT", "1")
+    else:
+        dev.set_option(OPT_SHAP_TABLE_MB, 0 if how == "cap0" else 1)
+    got = dev.predict(X, OUT_CONTRIB)
+    assert dev.info()["shap_table"] == -1
+    assert np.array_equal(got, want)
+    monkeypatch.delenv("TI_SHAP_TABLE_FAULT", raising=False)
+    assert np.array_equal(dev.predict(X, OUT_CONTRIB), want)    # still served, no retry
+
+
+def test_set_option_rejects_bad_values():
+    dev = DeviceForest(_xgb(4, 3, 5, seed=9), [0])
+    with pytest.raises(TreeInferError, match="unknown option"):
+        dev.set_option(99, 1)
+    with pytest.raises(TreeInferError, match=">= 0"):
+        dev.set_option(OPT_SHAP_TABLE_ROWS, -1)
 
 
 def test_deep_lightgbm_paths():
