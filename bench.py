@@ -394,17 +394,23 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
     pool = np.random.default_rng(seed + 1).standard_normal((64 * 1024, n_feat), dtype=np.float32)
     pool_ex = ThreadPoolExecutor(max_workers=2)
     lat = np.zeros(n_req)
+    done_at = np.zeros(n_req)
     batch_rows = []
     batch_ms = []
+    batch_span = []          # (loop time the batch was flushed, loop time its result was back)
+    lag = []                 # the load generator's wake-up lateness (event-loop stalls)
 
     async def predict_batch(instances):
         # the batcher concatenates the requests' matrices (as KFServer's
         # natively decoded bodies reach it); a list of rows is stacked
         X = instances if isinstance(instances, np.ndarray) else np.stack(instances)
         batch_rows.append(X.shape[0])
+        loop = asyncio.get_running_loop()
+        t0l = loop.time()
         t = time.perf_counter()
-        out = await asyncio.get_running_loop().run_in_executor(pool_ex, dev.predict, X)
+        out = await loop.run_in_executor(pool_ex, dev.predict, X)
         batch_ms.append((time.perf_counter() - t) * 1e3)
+        batch_span.append((t0l, loop.time()))
         return {"predictions": out}
 
     async def run_load():
@@ -420,7 +426,8 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
         tick = 2e-4
 
         def done(i, _fut):
-            lat[i] = loop.time() - arrivals[i]
+            done_at[i] = loop.time()
+            lat[i] = done_at[i] - arrivals[i]
 
         i = 0
         while i < n_req:
@@ -432,9 +439,12 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
                 futs.append(f)
                 i += 1
             if i < n_req:
-                await asyncio.sleep(max(tick, arrivals[i] - loop.time()))
+                want = max(tick, arrivals[i] - loop.time())
+                t_s = loop.time()
+                await asyncio.sleep(want)
+                lag.append(loop.time() - t_s - want)
         await asyncio.gather(*futs)
-        return loop.time() - t0
+        return loop.time() - t0, t0
 
     import gc
     old = gc.get_threshold()
@@ -443,7 +453,7 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
         from kfserving_amd.kfserving.kfserver import tune_gc
         tune_gc()
     try:
-        wall = asyncio.run(run_load())
+        wall, t_start = asyncio.run(run_load())
     finally:
         if freeze_gc:
             gc.unfreeze()
@@ -451,6 +461,17 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
             sys.setswitchinterval(old_si)
     pool_ex.shutdown()
     lat_ms = lat[warm:] * 1e3
+    # where the worst request's time went: the batch that answered it (its
+    # flush time and predict), the event loop's largest stall around it
+    iw = warm + int(np.argmax(lat_ms))
+    spans = np.asarray(batch_span)
+    bi = int(np.argmin(np.abs(spans[:, 1] - done_at[iw])))
+    arr_w = done_at[iw] - lat[iw]
+    worst = {"at_s": float(arr_w - t_start), "latency_ms": float(lat[iw] * 1e3),
+             "wait_to_flush_ms": float((spans[bi, 0] - arr_w) * 1e3),
+             "batch_predict_ms": float(batch_ms[bi]), "batch_rows": int(batch_rows[bi]),
+             "batch_index": bi, "max_loop_lag_ms": float(max(lag) * 1e3) if lag else None,
+             "requests_over_20ms": int((lat_ms > 20).sum())}
     return {"qps_offered": qps, "requests": n_req - warm, "rows_per_request": "U{1..64}",
             "max_batch_size": max_batch, "max_latency_ms": max_latency_ms,
             "p50_ms": float(np.percentile(lat_ms, 50)), "p99_ms": float(np.percentile(lat_ms, 99)),
@@ -459,6 +480,7 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
             "batches": len(batch_rows), "mean_batch_rows": float(np.mean(batch_rows)),
             "predict_ms_p50": float(np.percentile(batch_ms, 50)),
             "predict_ms_p99": float(np.percentile(batch_ms, 99)), "gc_frozen": freeze_gc,
+            "p999_ms": float(np.percentile(lat_ms, 99.9)), "worst": worst,
             "path": "in-process batcher -> ti_predict (host buffers), 1 GPU, no HTTP/JSON"}
 
 

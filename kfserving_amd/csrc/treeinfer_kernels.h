@@ -1822,6 +1822,9 @@ __global__ void __launch_bounds__(512) hexplicit_predict_kernel(const KArgs a) {
 // group runs for its deepest path), then the bottom in layout 7's lockstep.
 // KArgs: trees = image, depth = D0, rx_base = byte offset of each tree in the
 // image [T+1], rx_nint = internal nodes of each bottom [T].
+#ifndef TI_TX_MASK
+#define TI_TX_MASK 0
+#endif
 template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP, bool B8>
 __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t0, int t1,
                                          uint32_t sbase, uint32_t lane_off, int64_t row,
@@ -1885,7 +1888,13 @@ __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t
       for (int q = 0; q < ILP; ++q) {
         const uint32_t nx = rx_next<ZERO, SLOW, B8>(rec[q].x, rec[q].y, (uint16_t)b[q]);
         at[q] = in[q] ? nx : at[q];
+#if TI_TX_MASK
+        // only lanes that stepped read their new record (a lane at its leaf
+        // keeps the leaf's record: no random leaf-record read in the banking)
+        if (in[q]) rec[q] = lx_rec(base[q] + nx);
+#else
         rec[q] = lx_rec(base[q] + at[q]);
+#endif
       }
       if (__ballot(any) == 0) break;
     }
@@ -1954,6 +1963,9 @@ __global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
 // indexes the forest's position tables: the value (VIS) is loaded when the
 // group ends and added when the next group ends (tree order kept, the load's
 // latency hidden behind a walk); ordinals (leaf ids, vector leaves) at once.
+#ifndef TI_T8_MASK
+#define TI_T8_MASK 0
+#endif
 template <bool ZERO>
 __device__ __forceinline__ bool t8_right_slow(uint32_t x, uint32_t b) {
   using W = RxBins<true>;
@@ -2020,11 +2032,34 @@ __device__ __forceinline__ void t8_stage(const KArgs& a, ACC (&acc)[KMAX], int t
       x[q] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
           static_cast<uintptr_t>(base[q] + 4u * nd[q]));
     }
+#if TI_T8_MASK
+    // lanes at a leaf skip the step's reads (exec-masked: they take no part
+    // in the banking of the pair read, whose random leaf-pair addresses made
+    // most of the bank conflicts); the stale pair is the leaf's own pair, so
+    // the select still returns the leaf word, for any bin (see above)
+    uint32_t b[ILP];
+    rx_u2_t pr[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      b[q] = 1u;
+      pr[q].x = x[q];
+      pr[q].y = x[q];
+    }
+#endif
     for (;;) {
       uint32_t all = x[0];
 #pragma unroll
       for (int q = 1; q < ILP; ++q) all &= x[q];
       if (__ballot((all & W::kLeaf) == 0u) == 0) break;   // every lane of every tree at a leaf
+#if TI_T8_MASK
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        if ((x[q] & W::kLeaf) == 0u) {
+          b[q] = lds_u8((x[q] & W::kNodeMask) | lane_off);
+          pr[q] = lx_rec(base[q] + ((x[q] >> 24) << 3));
+        }
+      }
+#else
       uint32_t b[ILP];
       rx_u2_t pr[ILP];
 #pragma unroll
@@ -2032,6 +2067,7 @@ __device__ __forceinline__ void t8_stage(const KArgs& a, ACC (&acc)[KMAX], int t
         b[q] = lds_u8((x[q] & W::kNodeMask) | lane_off);
         pr[q] = lx_rec(base[q] + ((x[q] >> 24) << 3));
       }
+#endif
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
         if (!SLOW) {

@@ -2,6 +2,7 @@
 # A/B of the in-tree library against a variant build (TREEINFER_LIB) on the
 # kernel workloads of scripts/kernel_workload.py, interleaved, two rounds.
 # Build the variant with extra -D flags into kfserving_amd/lib/variants/NAME/
+# (python scripts/build_variant.py NAME -DFLAG=V ...)
 # (git-ignored), then: scripts/ab_variant.sh NAME OUT_SUBDIR [workloads...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 V=$(pwd)/kfserving_amd/lib/variants/$1/libtreeinfer.so
