@@ -281,10 +281,15 @@ class Application:
             X = v2.feature_matrix(v2.decode_inputs(req, tail))
         except v2.V2Error as e:
             return bad(str(e))
-        if self._batcher_factory is not None:
-            # one batcher per column count: a request of another width never
-            # lands in (and fails) a batch of well-formed ones; it fails alone
-            key = (name, "tensor", X.shape[1])
+        forest = getattr(model, "_forest", None)
+        width = getattr(forest, "n_features", None)
+        if self._batcher_factory is not None and (width is None or X.shape[1] == width):
+            # one tensor batcher per model, for requests of the model's own
+            # width; a request of another width (fewer columns read as missing,
+            # as the libraries read them) is predicted alone, so a client's
+            # widths can neither fail a batch of well-formed requests nor grow
+            # the batcher table
+            key = (name, "tensor")
             batcher = self._batchers.get(key)
             if batcher is None or batcher.model is not model:
                 batcher = self._batcher_factory(model, self._call, "tensor")

@@ -148,3 +148,95 @@ def test_c3_maxbin_full_float64():
     X32 = X[:50_000].astype(np.float32)
     assert np.array_equal(dev.predict(X32, OUT_MARGIN),
                           port.lgb_predict_raw(trees, 1, 100, X32.astype(np.float64))[:, 0])
+
+
+def _lgb_to_xgb_raw(t):
+    """A LightGBM tree dict as XGBoost RegTree arrays (internal nodes 0..n-1,
+    then the leaves; default_left from decision_type bit 1): an irregular,
+    deep, <= 255-leaf tree with a float32 accumulator."""
+    sf = np.asarray(t["split_feature"], np.int64)
+    n_int = sf.shape[0]
+    lv = np.asarray(t["leaf_value"], np.float64)
+    n = n_int + lv.shape[0]
+    cleft = np.full(n, -1, np.int32)
+    cright = np.full(n, -1, np.int32)
+    fix = lambda c: c if c >= 0 else n_int + (~c)          # noqa: E731
+    for i in range(n_int):
+        cleft[i] = fix(int(t["left_child"][i]))
+        cright[i] = fix(int(t["right_child"][i]))
+    dl = (np.asarray(t["decision_type"], np.int64) >> 1) & 1
+    sindex = np.zeros(n, np.uint32)
+    sindex[:n_int] = sf.astype(np.uint32) | (dl.astype(np.uint32) << 31)
+    value = np.zeros(n, np.float32)
+    value[:n_int] = np.asarray(t["threshold"], np.float64).astype(np.float32)
+    value[n_int:] = (lv * 0.1).astype(np.float32)
+    return {"cleft": cleft, "cright": cright, "sindex": sindex, "value": value}
+
+
+@pytest.mark.parametrize("tx8", [1, 0])
+def test_u8_multiclass_lightgbm(monkeypatch, tx8):
+    """K = 3 output groups on u8 bins (the deferred leaf adds of the
+    compact bottom land in tree_group t mod 3), raw scores and leaf ids bit
+    exact against the C port."""
+    monkeypatch.setenv("TI_TX8", str(tx8))
+    trees = lf.synthetic_maxbin_trees(45, 200, 20, seed=31)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "model.txt")
+        lf.write_lightgbm_text(p, trees, 20, "multiclass num_class:3", num_class=3)
+        f = load_lightgbm_model(p)
+    dev = DeviceForest(f, [0])
+    info = dev.info()
+    assert info["layout"] == TEXPLICIT and info["bin_bits"] == 8 and info["bottom"] == tx8
+    X = _inputs(trees, 2500, 20, seed=32, special_frac=0.01)
+    for Xi in (X, X.astype(np.float32)):
+        want = port.lgb_predict_raw(trees, 3, 20, Xi.astype(np.float64))
+        assert np.array_equal(dev.predict(Xi, OUT_MARGIN), want)
+
+
+@pytest.mark.parametrize("tx8", [1, 0])
+def test_u8_float32_accumulator_xgboost(monkeypatch, tx8):
+    """a float32-accumulating forest (XGBoost, 4-byte leaf table of
+    the compact bottom) on u8 bins: deep irregular trees of <= 255 leaves with
+    at most 254 distinct thresholds a feature; margins bit-exact against the
+    xgboost restatement."""
+    from kfserving_amd.formats.xgboost_format import forest_from_raw_trees
+    from oracle import xgb_ref
+    monkeypatch.setenv("TI_TX8", str(tx8))
+    lt = lf.synthetic_maxbin_trees(40, 255, 16, seed=33)
+    raw = [_lgb_to_xgb_raw(t) for t in lt]
+    ti = np.zeros(len(raw), np.int32)
+    f = forest_from_raw_trees(raw, ti, 16, 0, 0.0, "binary:logistic")
+    ref = xgb_ref.from_raw_trees(raw, ti, 16, 0, 0.0, "binary:logistic")
+    dev = DeviceForest(f, [0])
+    info = dev.info()
+    assert info["layout"] == TEXPLICIT and info["bin_bits"] == 8 and info["bottom"] == tx8
+    X = _inputs(lt, 3000, 16, seed=34, special_frac=0.01).astype(np.float32)
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), xgb_ref.predict(ref, X, output_margin=True))
+    assert np.array_equal(dev.predict(X, OUT_LEAF), xgb_ref.leaf_index(ref, X))
+
+
+def test_u8_vector_leaves_sklearn_classifier(monkeypatch):
+    """vector leaves (leaf_width = K) through the compact bottom's
+    ordinal table: a sklearn RandomForestClassifier, 3 classes, depth up to 14,
+    <= 200 leaves a tree, features of <= 60 distinct values (u8 bins);
+    predict_proba bit-exact against sklearn itself and the u16 image."""
+    from sklearn.ensemble import RandomForestClassifier
+    from kfserving_amd.forest import OUT_PREDICT
+    from kfserving_amd.formats.sklearn_format import forest_from_sklearn
+    rng = np.random.default_rng(35)
+    Xt = rng.integers(0, 60, (4000, 12)).astype(np.float32)
+    y = ((Xt[:, 0] + Xt[:, 1] * 0.5 + rng.normal(0, 8, 4000)) // 30).astype(int) % 3
+    est = RandomForestClassifier(n_estimators=12, max_depth=14, max_leaf_nodes=200,
+                                 random_state=0).fit(Xt, y)
+    f = forest_from_sklearn(est)
+    monkeypatch.setenv("TI_FORCE_LAYOUT", "texplicit")
+    d8 = _device(f, monkeypatch, True)
+    d16 = _device(f, monkeypatch, False)
+    info = d8.info()
+    assert info["layout"] == TEXPLICIT and info["bin_bits"] == 8 and info["bottom"] == 1, info
+    X = rng.integers(-2, 62, (3000, 12)).astype(np.float32)
+    X[rng.random(X.shape) < 0.01] = np.nan
+    want = est.predict_proba(X)
+    got = d8.predict(X, OUT_PREDICT)
+    np.testing.assert_array_equal(got.reshape(want.shape), want)
+    assert np.array_equal(got, d16.predict(X, OUT_PREDICT))

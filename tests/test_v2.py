@@ -212,3 +212,26 @@ def test_v2_decode_errors_are_v2_errors():
     for req, tail in cases:
         with pytest.raises(v2.V2Error):
             v2.decode_inputs(req, tail)
+
+
+def test_v2_tensor_widths_do_not_grow_batchers(serve):
+    """requests of any width are answered, but only the model's own
+    width is batched; other widths are predicted alone, so a client cannot
+    create a batcher per width."""
+    class Forest:
+        n_features = 3
+
+    m = RowSum()
+    m._forest = Forest()
+    server = KFServer(registered_models=KFModelRepository(), max_batchsize=16, max_latency_ms=5)
+    server.register_model(m)
+    apps = []
+    make = server.create_application
+    server.create_application = lambda: apps.append(make()) or apps[-1]
+    s = serve(server)
+    for w in (3, 2, 5, 7, 3, 11):
+        req = {"inputs": [{"name": "x", "shape": [1, w], "datatype": "FP64", "data": [1.0] * w}]}
+        code, _, out = s.fetch("/v2/models/m/infer", "POST", json.dumps(req).encode())
+        assert code == 200, out
+        assert json.loads(out)["outputs"][0]["data"] == [2.0 * w]
+    assert [k for k in apps[0]._batchers if "tensor" in k] == [("m", "tensor")]
