@@ -309,7 +309,8 @@ def synthetic_leafwise_trees(n_trees: int, num_leaves: int, n_features: int, see
                              missing_types=(MISSING_NONE, MISSING_ZERO, MISSING_NAN)) -> List[dict]:
     """Seeded leaf-wise trees: grow by splitting a
     random current leaf until ``num_leaves``; thresholds ~ N(0,1) as float64,
-    decision_type draws default_left and a missing type."""
+    decision_type draws default_left and a missing type; leaf / internal
+    counts are those of a seeded N(0,1) sample (plus one per leaf)."""
     rng = np.random.default_rng(seed)
     crng = np.random.default_rng([seed, 7919])
     trees = []
@@ -338,7 +339,18 @@ def synthetic_leafwise_trees(n_trees: int, num_leaves: int, n_features: int, see
             leaf_owner.append((node, 1))
             left[node] = ~j
             right[node] = ~new_leaf
-        leaf_count = crng.integers(1, 200, size=num_leaves)   # own stream: trees unchanged
+        # counts as training would leave them: the rows of a seeded N(0,1)
+        # sample that reach each leaf (+ 1: leaf-wise growth never leaves one
+        # empty), from the counts' own stream (the trees are unchanged)
+        Xs = crng.standard_normal((2000, n_features))
+        node = np.zeros(Xs.shape[0], dtype=np.int64)
+        rows = np.arange(Xs.shape[0])
+        while (node >= 0).any():
+            live = node >= 0
+            nd = node[live]
+            go_left = Xs[rows[live], feat[nd]] <= thr[nd]
+            node[live] = np.where(go_left, left[nd], right[nd])
+        leaf_count = np.bincount(~node, minlength=num_leaves).astype(np.int64) + 1
         internal_count = np.zeros(n_int, dtype=np.int64)
 
         def count(c):
