@@ -186,7 +186,7 @@ def test_bheap_fixed_walk(quantize, ng):
     env = {"TI_BHEAP_NG": ng}
     dev = _with_env(env, lambda: DeviceForest(forest, [0]))
     inf = dev.info()
-    assert inf["layout"] == BHEAP and inf["walk"] == 1 and inf["depth"] == 8
+    assert inf["layout"] == BHEAP and inf["walk"] == 2 and inf["depth"] == 8
     assert inf["bin_bits"] == (8 if quantize else 16)
     for rows in (1, 511, 512, 513, 4097):
         X = _edge_rows(deep, 8, 28, rows, seed=rows + 3)
@@ -205,7 +205,7 @@ def test_bheap_fixed_walk(quantize, ng):
     f3 = xf.forest_from_raw_trees(trees3, ti3, 28, 3, 0.5, "multi:softprob")
     r3 = xgb_ref.from_raw_trees(trees3, ti3, 28, 3, 0.5, "multi:softprob")
     d3 = _with_env(env, lambda: DeviceForest(f3, [0]))
-    assert d3.info()["walk"] == 1
+    assert d3.info()["walk"] == 2
     X = _edge_rows(trees3, 8, 28, 2049, seed=11)
     assert np.array_equal(_with_env(env, lambda: d3.predict(X, OUT_MARGIN)),
                           xgb_ref.predict(r3, X, output_margin=True))
