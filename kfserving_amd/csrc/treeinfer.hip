@@ -529,6 +529,7 @@ struct DeviceForest {
   int32_t* tree_group = nullptr;
   // binned heap layout: one image + threshold tables per input dtype
   unsigned char* bh_img[2] = {nullptr, nullptr};
+  unsigned char* bh_fix_img = nullptr;   // the fixed walk's permuted image (fix_permute)
   unsigned char* bh_tbl[2] = {nullptr, nullptr};
   // record layouts (6-9): rank tables per input dtype
   unsigned char* bx_tbl[2] = {nullptr, nullptr};
@@ -591,6 +592,7 @@ struct ti_forest {
   // float32 view round_down_f32(t), float64 view t)
   struct BinImage {
     std::vector<unsigned char> img;   // [T][stride]
+    std::vector<unsigned char> fix_img;   // img with hot pair slots first (fix_permute), or empty
     std::vector<unsigned char> tbl;   // [F][2^L] XT Eytzinger tables, or 5-ary (kary > 0)
     int32_t L = 0;
     int32_t kary = 0;                 // > 0: tbl holds float32 5-ary tables of this height
@@ -697,7 +699,7 @@ void free_device(DeviceForest& d) {
   (void)hipSetDevice(d.device);
   void* ptrs[] = {d.heap32, d.heap64, d.heap_leaf_ids, d.nodes, d.thr64, d.node_base, d.root,
                   d.leaf_base, d.leaves, d.exp_leaf_ids, d.tree_group, d.x_buf, d.out_buf,
-                  d.cat_words, d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1],
+                  d.cat_words, d.bh_img[0], d.bh_img[1], d.bh_tbl[0], d.bh_tbl[1], d.bh_fix_img,
                   d.bx_tbl[0], d.bx_tbl[1],
                   d.shap_paths, d.shap_elems, d.shap_leaf, d.shap_bias, d.shap_tab, d.shap_tab_off,
                   d.rx_recs[0], d.rx_recs[1], d.rx_base, d.rx_nint, d.lx_stage,
@@ -728,6 +730,7 @@ void free_device(DeviceForest& d) {
   d.leaves = d.x_buf = d.out_buf = nullptr;
   d.cat_words = nullptr;
   for (int i = 0; i < 2; ++i) d.bh_img[i] = d.bh_tbl[i] = d.bx_tbl[i] = nullptr;
+  d.bh_fix_img = nullptr;
   d.rx_recs[0] = d.rx_recs[1] = nullptr;
   d.rx_base = d.rx_nint = nullptr;
   d.lx_stage = nullptr;
@@ -1078,6 +1081,42 @@ void kary_tables(const RankTables<XT>& rt, std::vector<unsigned char>* out, int*
   *height = H;
 }
 
+// The fixed walk (bheap_fix_kernel) finds a node's children pair through the
+// pair slot the node word carries in bits 3..10, not by heap arithmetic, so
+// within a level the slots may be any permutation.  fix_permute numbers each
+// level's nodes by cover, largest first: the lanes of a wave, which crowd onto
+// the nodes the training rows took, then read pairs packed at the start of the
+// level's slots -- the same address (a broadcast) or nearby dwords -- instead
+// of pairs up to 1 KB apart whose dwords collide in the LDS banks.  Same
+// words, same walk, same sums; only the fixed walk reads this image (leaf ids
+// keep the heap-indexed walk on img).
+void fix_permute(ti_forest::BinImage* bi, const std::vector<double>& hcov, int NE) {
+  const int64_t T = static_cast<int64_t>(bi->img.size()) / bi->stride;
+  bi->fix_img.assign(bi->img.size(), 0);
+  std::vector<int32_t> pi(NE, 0), lvl;
+  for (int64_t t = 0; t < T; ++t) {
+    const uint32_t* on = reinterpret_cast<const uint32_t*>(bi->img.data() + bi->stride * t);
+    const float* ol = reinterpret_cast<const float*>(on + NE);
+    uint32_t* nn = reinterpret_cast<uint32_t*>(bi->fix_img.data() + bi->stride * t);
+    float* nl = reinterpret_cast<float*>(nn + NE);
+    const double* c = hcov.data() + static_cast<size_t>(t) * NE;
+    for (int lo = 1; lo < NE; lo <<= 1) {   // level [lo, 2 lo): slots by cover
+      lvl.resize(lo);
+      for (int i = 0; i < lo; ++i) lvl[i] = lo + i;
+      std::stable_sort(lvl.begin(), lvl.end(), [c](int32_t x, int32_t y) { return c[x] > c[y]; });
+      for (int i = 0; i < lo; ++i) pi[lvl[i]] = lo + i;
+    }
+    auto relabel = [&](uint32_t w, int h) { return (w & ~0x7F8u) | (static_cast<uint32_t>(pi[h]) << 3); };
+    nn[1] = relabel(on[1], 1);
+    for (int v = 1; v < NE; ++v)
+      for (int s = 0; s < 2; ++s) {
+        const int ch = 2 * v + s, nw = 2 * pi[v] + s;
+        if (ch < NE) nn[nw] = relabel(on[ch], ch);
+        else nl[nw - NE] = ol[ch - NE];
+      }
+  }
+}
+
 template <typename XT, typename ACC>
 bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
                 std::vector<int32_t>* leaf_ids) {
@@ -1122,18 +1161,24 @@ bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
   bi->stride = static_cast<int64_t>(align16(sizeof(uint32_t) * NE + sizeof(ACC) * NE * LW));
   bi->img.assign(static_cast<size_t>(bi->stride) * d->n_trees, 0);
   if (leaf_ids) leaf_ids->assign(static_cast<size_t>(NE) * d->n_trees, 0);
-  struct Item { int32_t node; int32_t heap; int32_t level; };
+  struct Item { int32_t node; int32_t heap; int32_t level; double cov; };
   std::vector<Item> st;
+  // the fixed walk's permuted image (fix_permute): float32 view, 512-row
+  // tiles, depth-8 records of float leaves, covers in the model
+  const bool perm = sizeof(XT) == 4 && sizeof(ACC) == 4 && with_index && D == 8 && LW == 1 && d->cover &&
+                    env_int("TI_FIX_PERM", 1) != 0;
+  std::vector<double> hcov(perm ? static_cast<size_t>(NE) * d->n_trees : 0, 0.0);
   for (int t = 0; t < d->n_trees; ++t) {
     unsigned char* rec = bi->img.data() + static_cast<size_t>(bi->stride) * t;
     uint32_t* nodes = reinterpret_cast<uint32_t*>(rec);
     ACC* leaves = reinterpret_cast<ACC*>(rec + sizeof(uint32_t) * NE);
     const int64_t b = d->tree_offset[t];
-    st.assign(1, Item{0, 1, 0});
+    st.assign(1, Item{0, 1, 0, d->cover ? d->cover[b] : 0.0});
     while (!st.empty()) {
       const Item it = st.back();
       st.pop_back();
       const int64_t g = b + it.node;
+      if (perm && it.level < D) hcov[static_cast<size_t>(t) * NE + it.heap] = it.cov;
       if (it.level == D) {
         const int slot = it.heap - NE;
         for (int k = 0; k < LW; ++k)
@@ -1144,15 +1189,18 @@ bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
       const uint32_t idx = with_index ? static_cast<uint32_t>(it.heap) << 3 : 0u;
       if (d->feature[g] < 0) {   // shallow leaf: always-left padding down to level D
         nodes[it.heap] = (0xFFFFu << 16) | idx;
-        st.push_back(Item{it.node, 2 * it.heap, it.level + 1});
-        st.push_back(Item{it.node, 2 * it.heap + 1, it.level + 1});
+        st.push_back(Item{it.node, 2 * it.heap, it.level + 1, it.cov});
+        st.push_back(Item{it.node, 2 * it.heap + 1, it.level + 1, 0.0});
       } else {
         nodes[it.heap] = node_word(g) | idx;
-        st.push_back(Item{d->left[g], 2 * it.heap, it.level + 1});
-        st.push_back(Item{d->right[g], 2 * it.heap + 1, it.level + 1});
+        st.push_back(Item{d->left[g], 2 * it.heap, it.level + 1,
+                          d->cover ? d->cover[b + d->left[g]] : 0.0});
+        st.push_back(Item{d->right[g], 2 * it.heap + 1, it.level + 1,
+                          d->cover ? d->cover[b + d->right[g]] : 0.0});
       }
     }
   }
+  if (perm) fix_permute(bi, hcov, NE);
   return true;
 }
 
@@ -1904,6 +1952,7 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
   } else if (f->layout == 3) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.bh_img[i], f->bh[i].img, &d.bytes))) return rc;
+    if ((rc = upload(&d.bh_fix_img, f->bh[0].fix_img, &d.bytes))) return rc;
       if ((rc = upload(&d.bh_tbl[i], f->bh[i].tbl, &d.bytes))) return rc;
     }
     if ((rc = upload(&d.heap_leaf_ids, f->h_heap_leaf_ids, &d.bytes))) return rc;
@@ -2163,6 +2212,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.trees = d.bh_img[ii];
     a.tree_stride = stride_b;
     a.heap_leaf_ids = d.heap_leaf_ids;
+    const bool fix_perm = d.bh_fix_img != nullptr && bheap_fixed(f, xdt, kind);
     a.depth = f->depth;
     a.stage_trees = static_cast<int32_t>(S);
     a.bin_tbl = d.bh_tbl[ii];
@@ -2183,6 +2233,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
       a.stage_trees = 4 * ng;
       a.bin_chunk = 4 * ng;
       a.stage_off = static_cast<int32_t>(ti::kFixStage);
+      if (fix_perm) a.trees = d.bh_fix_img;   // same walk, hot pair slots first
       lds = ti::kFixStage + static_cast<size_t>(4 * ng) * ti::kFixTree;
     }
     int rc = ensure_lds_attr(d.device, fn);
@@ -3178,6 +3229,8 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   for (auto& bi : f->bh) {
     bi.img.clear();
     bi.img.shrink_to_fit();
+    bi.fix_img.clear();
+    bi.fix_img.shrink_to_fit();
     bi.tbl.clear();
     bi.tbl.shrink_to_fit();
   }

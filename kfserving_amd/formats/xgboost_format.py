@@ -396,7 +396,8 @@ def synthetic_complete_trees(n_trees: int, depth: int, n_features: int, seed: in
     """Seeded complete depth-``depth`` XGBoost trees.
 
     feature ~ U{0..F-1}, threshold ~ N(0,1) rounded to float32, default_left ~
-    Bernoulli(1/2), leaf ~ U(-0.05, 0.05) float32; nodes numbered in heap order.
+    Bernoulli(1/2), leaf ~ U(-0.05, 0.05) float32; nodes numbered in heap order;
+    sum_hess (the covers) from a seeded N(0,1) sample.
     """
     rng = np.random.default_rng(seed)
     crng = np.random.default_rng([seed, 7919])   # covers: own stream, trees unchanged
@@ -416,9 +417,17 @@ def synthetic_complete_trees(n_trees: int, depth: int, n_features: int, seed: in
         value = np.zeros(n, dtype=np.float32)
         value[:n_int] = rng.standard_normal(n_int).astype(np.float32)
         value[n_int:] = rng.uniform(-0.05, 0.05, size=n - n_int).astype(np.float32)
-        # covers: leaf hessian sums ~ U(1, 100), a parent the float32 sum of its children
+        # covers as training on N(0,1) rows leaves them: the logistic hessian
+        # sum p(1 - p) ~ 0.25 per row of a seeded N(0,1) sample reaching each
+        # leaf (+ 1 row: no empty leaf), a parent the float32 sum of its
+        # children; from the covers' own stream (the trees are unchanged)
+        Xs = crng.standard_normal((2000, n_features)).astype(np.float32)
+        node = np.zeros(Xs.shape[0], dtype=np.int64)
+        for _ in range(depth):
+            go_left = ~(Xs[np.arange(Xs.shape[0]), feat[node]] >= value[node])   # x < t or NaN
+            node = np.where(go_left, cleft[node], cright[node])
         hess = np.zeros(n, dtype=np.float32)
-        hess[n_int:] = crng.uniform(1.0, 100.0, size=n - n_int).astype(np.float32)
+        hess[n_int:] = (0.25 * (np.bincount(node - n_int, minlength=n - n_int) + 1)).astype(np.float32)
         for i in range(n_int - 1, -1, -1):
             hess[i] = hess[2 * i + 1] + hess[2 * i + 2]
         trees.append({"cleft": cleft, "cright": cright, "sindex": sindex, "value": value,
