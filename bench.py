@@ -75,7 +75,7 @@ WALK_KERNELS = {0: "bheap_predict_kernel", 1: "bheap_fix_kernel", 2: "bheap_fix_
 # (scripts/kernel_pmc.sh -> scripts/make_pmc_json.py)
 PMC_PASSES = {"c2": "profiles/pmc_c2.json", "c3": "profiles/r3_c3_pmc.json",
               "c3_f64": "profiles/r3_c3_f64_pmc.json", "c3_maxbin": "profiles/r3_c3_maxbin_pmc.json",
-              "c4": "profiles/r3_c4_pmc.json"}
+              "c4": "profiles/r3_c4_pmc.json", "c2_hist": "profiles/r4_c2_hist_pmc.json"}
 
 
 def pmc_path(key: str) -> str:
@@ -130,7 +130,7 @@ def parse_args(argv=None):
     p.add_argument("--latency-qps", type=float, default=10000.0,
                    help="offered requests/s for the batched-latency leg (0 = skip)")
     p.add_argument("--latency-seconds", type=float, default=3.0)
-    p.add_argument("--configs", default="c3,c3_f64,c3_maxbin,c4",
+    p.add_argument("--configs", default="c3,c3_f64,c3_maxbin,c4,c2_hist",
                    help="other named configs to time after the headline ('' = none)")
     p.add_argument("--rows3", type=int, default=100_000_000)
     p.add_argument("--rows4", type=int, default=10_000_000)
@@ -529,6 +529,17 @@ def _lgb_forest(trees, what):
         return lf.load_lightgbm_model(p), trees, what
 
 
+def c2_hist_forest():
+    """C2's shape as xgboost's hist / approx tree methods train it: the same
+    draws with every threshold on the nearest of 253 N(0,1) quantile bin
+    bounds (max_bin 254), so at most 253 thresholds a feature and u8 bins."""
+    from kfserving_amd.formats.xgboost_format import (forest_from_raw_trees,
+                                                      synthetic_complete_trees)
+    trees, ti = synthetic_complete_trees(N_TREES, DEPTH, N_FEAT, seed=0, max_bin=254)
+    return (forest_from_raw_trees(trees, ti, N_FEAT, 0, 0.0, "binary:logistic"), (trees, ti),
+            "XGBoost binary:logistic, 500 x depth 8, thresholds on 253 quantile bin bounds")
+
+
 def c3_forest():
     from kfserving_amd.formats import lightgbm_format as lf
     return _lgb_forest(lf.synthetic_leafwise_trees(1000, 255, 100, seed=1),
@@ -786,6 +797,13 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             if r is not None:
                 r.update(config=f"C3 LightGBM leaf-wise 1000 trees x 255 leaves, 100 features, "
                                 f"{dt} input, float64 sigmoid of the raw score", model=src)
+        elif name == "c2_hist":
+            f2, _, src = c2_hist_forest()
+            r = run_config(f2, N_FEAT, args.rows, 4, args, world, rank, device, dev_sync,
+                           make_engine, None, "c2_hist", pmc_path("c2_hist"))
+            if r is not None:
+                r.update(config="C2 shape, hist-trained thresholds (u8 bins): 500 trees depth 8, "
+                                "28 features, float32 input, float32 sums", model=src)
         elif name == "c4":
             f4, raw4, src = c4_forest()
             r = run_config(f4, 64, args.rows4, 2, args, world, rank, device, dev_sync,

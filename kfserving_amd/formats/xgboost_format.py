@@ -392,13 +392,22 @@ def write_json_model(path: str, trees: List[dict], tree_info, num_feature: int, 
 
 
 def synthetic_complete_trees(n_trees: int, depth: int, n_features: int, seed: int,
-                             num_class: int = 0) -> Tuple[List[dict], np.ndarray]:
+                             num_class: int = 0, max_bin: int = 0) -> Tuple[List[dict], np.ndarray]:
     """Seeded complete depth-``depth`` XGBoost trees.
 
     feature ~ U{0..F-1}, threshold ~ N(0,1) rounded to float32, default_left ~
     Bernoulli(1/2), leaf ~ U(-0.05, 0.05) float32; nodes numbered in heap order;
-    sum_hess (the covers) from a seeded N(0,1) sample.
+    sum_hess (the covers) from a seeded N(0,1) sample.  ``max_bin`` > 0 snaps
+    every threshold to the nearest of the max_bin - 1 N(0,1) quantile edges
+    Phi^-1(k / max_bin), as xgboost's hist / approx tree methods place splits
+    on histogram bin bounds (at most max_bin - 1 distinct thresholds a
+    feature: u8 bins in the engine); the draws are the same either way.
     """
+    edges = None
+    if max_bin > 0:
+        from statistics import NormalDist
+        nd = NormalDist()
+        edges = np.array([nd.inv_cdf(k / max_bin) for k in range(1, max_bin)], dtype=np.float32)
     rng = np.random.default_rng(seed)
     crng = np.random.default_rng([seed, 7919])   # covers: own stream, trees unchanged
     n_int = (1 << depth) - 1
@@ -416,6 +425,8 @@ def synthetic_complete_trees(n_trees: int, depth: int, n_features: int, seed: in
         sindex[:n_int] = feat | (dl << 31)
         value = np.zeros(n, dtype=np.float32)
         value[:n_int] = rng.standard_normal(n_int).astype(np.float32)
+        if edges is not None:
+            value[:n_int] = edges[np.abs(value[:n_int, None] - edges[None, :]).argmin(axis=1)]
         value[n_int:] = rng.uniform(-0.05, 0.05, size=n - n_int).astype(np.float32)
         # covers as training on N(0,1) rows leaves them: the logistic hessian
         # sum p(1 - p) ~ 0.25 per row of a seeded N(0,1) sample reaching each

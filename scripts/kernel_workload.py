@@ -4,6 +4,7 @@ N(0,1) batch of bench.py's config, --steps launches of OUT_PREDICT on the
 launch stream, one JSON line with the event time per launch.
 
   c2         500 x depth-8 XGBoost binary, 28 features, float32 (bench headline)
+  c2_hist    the same trees with hist-style thresholds (253 quantile bounds: u8 bins)
   c3 / c3_f64  LightGBM leaf-wise 1000 x 255 leaves, 100 features, float32 /
              float64 input (lgbserver's DataFrame dtype)
   c3_maxbin  the LightGBM-shaped variant (thresholds on 255 quantile bin edges,
@@ -25,6 +26,8 @@ def forest_of(workload):
     import bench
     if workload == "c2":
         return bench.build_model()[2], bench.N_FEAT, "float32"
+    if workload == "c2_hist":
+        return bench.c2_hist_forest()[0], bench.N_FEAT, "float32"
     if workload in ("c3", "c3_f64"):
         return bench.c3_forest()[0], 100, "float64" if workload == "c3_f64" else "float32"
     if workload == "c3_maxbin":
