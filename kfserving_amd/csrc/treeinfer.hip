@@ -549,7 +549,7 @@ struct DeviceForest {
   double* shap_bias = nullptr;
   void* shap_tab = nullptr;          // TreeSHAP coefficient table (shap_table_kernel), MT-typed
   int64_t* shap_tab_off = nullptr;   // [paths] first coefficient of each path
-  int32_t shap_tab_state = 0;        // 0 not tried, 1 built, -1 failed or over the cap:
+  std::atomic<int32_t> shap_tab_state{0};   // 0 not tried, 1 built, -1 failed or over the cap:
                                      // contributions use the extend / unwind kernel
   // ti_predict scratch: device buffers + pinned host staging (grown x2)
   void* x_buf = nullptr;
@@ -3275,7 +3275,7 @@ int ti_forest_get_info(const ti_forest* f, ti_forest_info* info) {
   info->bottom = f->layout == 9 ? f->tx8 : 0;
   // the TreeSHAP coefficient table of slot 0 (of the first part)
   const ti_forest* sf = f->parts.empty() ? f : f->parts[0].get();
-  info->shap_table = sf->devs.empty() ? 0 : sf->devs[0]->shap_tab_state;
+  info->shap_table = sf->devs.empty() ? 0 : sf->devs[0]->shap_tab_state.load();
   info->reserved1 = 0;
   info->shap_table_bytes = info->shap_table == 1 ? sf->shap_tab_len * sf->shap_tab_mt : 0;
   info->shap_table_build_ms = sf->shap_tab_build_ms;
