@@ -422,12 +422,20 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
         loop = asyncio.get_running_loop()
         t0 = loop.time() + 0.05
         arrivals = t0 + np.cumsum(gaps)
-        futs = []
         tick = 2e-4
+        all_done = asyncio.Event()
+        n_done = [0]
 
+        # completion is counted in the callbacks: an asyncio.gather over the
+        # ~35k futures at the end blocked the loop thread for ~35-45 ms
+        # (attaching a callback to each), which held back the last batch's
+        # flush timer and was round 3's unexplained 50 ms max_ms
         def done(i, _fut):
             done_at[i] = loop.time()
             lat[i] = done_at[i] - arrivals[i]
+            n_done[0] += 1
+            if n_done[0] == n_req:
+                all_done.set()
 
         i = 0
         while i < n_req:
@@ -436,14 +444,13 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
                 off = (i * 64) % (len(pool) - 64)
                 f = b.enqueue(pool[off:off + int(sizes[i])])
                 f.add_done_callback(functools.partial(done, i))
-                futs.append(f)
                 i += 1
             if i < n_req:
                 want = max(tick, arrivals[i] - loop.time())
                 t_s = loop.time()
                 await asyncio.sleep(want)
                 lag.append(loop.time() - t_s - want)
-        await asyncio.gather(*futs)
+        await all_done.wait()
         return loop.time() - t0, t0
 
     import gc

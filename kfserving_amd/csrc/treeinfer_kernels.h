@@ -919,14 +919,9 @@ __device__ __forceinline__ void fix_step(uint32_t& nd, uint32_t b, uint2 pr) {
         : "vcc", "scc");
   }
 }
-#ifndef TI_FIX_VBIN
-#define TI_FIX_VBIN 0
-#endif
-constexpr int kFixWords = 14;   // bin words the fixed walk allows (host: <= 14)
 template <int KMAX, bool B16, bool CHECK_NAN, int NG>
 __device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0, float (&acc)[KMAX],
-                                                uint32_t lane_off, const u32x4 (&top)[4 * NG],
-                                                const uint32_t (&vbin)[kFixWords]) {
+                                                uint32_t lane_off, const u32x4 (&top)[4 * NG]) {
   const uint32_t bmask = a.bin_mask;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
@@ -935,21 +930,8 @@ __device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0,
 #if TI_FIX_SROOT
     {
       uint32_t b0[4];
-#if TI_FIX_VBIN
-      // level 0's feature is wave-uniform (the scalar root), so its bin comes
-      // from the lane's bin words held in VGPRs (a uniform-index register
-      // read) instead of an LDS read: one LDS instruction of 15 a tree fewer
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t off = top[g * 4 + q].y & bmask;   // word * R * 4 + byte
-        const uint32_t w = __builtin_amdgcn_readfirstlane(off >> 11);
-        const uint32_t sh = __builtin_amdgcn_readfirstlane((off & 3u) * 8u);
-        b0[q] = (vbin[w] >> sh) & (B16 ? 0xFFFFu : 0xFFu);
-      }
-#else
 #pragma unroll
       for (int q = 0; q < 4; ++q) b0[q] = lds_bin<B16>((top[g * 4 + q].y & bmask) | lane_off);
-#endif
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const u32x4 tp = top[g * 4 + q];
@@ -1020,10 +1002,6 @@ __global__ void __launch_bounds__(512) bheap_fix_kernel(const KArgs a) {
   float acc[KMAX];
   init_acc(acc, a);
   u32x4 top[4 * NG] = {};
-  uint32_t vbin[kFixWords];   // the lane's bin words (TI_FIX_VBIN)
-#pragma unroll
-  for (int w = 0; w < kFixWords; ++w)
-    vbin[w] = TI_FIX_VBIN && w < a.bin_words ? lds_u32((uint32_t)(w * R * 4) + lane_off) : 0u;
   for (int t0 = 0; t0 < T; t0 += S) {
     const int cnt = (T - t0) < S ? (T - t0) : S;
     __syncthreads();
@@ -1042,9 +1020,9 @@ __global__ void __launch_bounds__(512) bheap_fix_kernel(const KArgs a) {
       }
     }
     if (tile_nan)
-      bheap_fix_stage<KMAX, B16, true, NG>(a, cnt, t0, acc, lane_off, top, vbin);
+      bheap_fix_stage<KMAX, B16, true, NG>(a, cnt, t0, acc, lane_off, top);
     else
-      bheap_fix_stage<KMAX, B16, false, NG>(a, cnt, t0, acc, lane_off, top, vbin);
+      bheap_fix_stage<KMAX, B16, false, NG>(a, cnt, t0, acc, lane_off, top);
   }
   if (!live) return;
   finish_row<float, KMAX>(acc, a, row);
@@ -1844,9 +1822,6 @@ __global__ void __launch_bounds__(512) hexplicit_predict_kernel(const KArgs a) {
 // group runs for its deepest path), then the bottom in layout 7's lockstep.
 // KArgs: trees = image, depth = D0, rx_base = byte offset of each tree in the
 // image [T+1], rx_nint = internal nodes of each bottom [T].
-#ifndef TI_TX_MASK
-#define TI_TX_MASK 0
-#endif
 template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP, bool B8>
 __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t0, int t1,
                                          uint32_t sbase, uint32_t lane_off, int64_t row,
@@ -1910,13 +1885,7 @@ __device__ __forceinline__ void tx_stage(const KArgs& a, ACC (&acc)[KMAX], int t
       for (int q = 0; q < ILP; ++q) {
         const uint32_t nx = rx_next<ZERO, SLOW, B8>(rec[q].x, rec[q].y, (uint16_t)b[q]);
         at[q] = in[q] ? nx : at[q];
-#if TI_TX_MASK
-        // only lanes that stepped read their new record (a lane at its leaf
-        // keeps the leaf's record: no random leaf-record read in the banking)
-        if (in[q]) rec[q] = lx_rec(base[q] + nx);
-#else
         rec[q] = lx_rec(base[q] + at[q]);
-#endif
       }
       if (__ballot(any) == 0) break;
     }
@@ -1985,9 +1954,6 @@ __global__ void __launch_bounds__(512) texplicit_predict_kernel(const KArgs a) {
 // indexes the forest's position tables: the value (VIS) is loaded when the
 // group ends and added when the next group ends (tree order kept, the load's
 // latency hidden behind a walk); ordinals (leaf ids, vector leaves) at once.
-#ifndef TI_T8_MASK
-#define TI_T8_MASK 0
-#endif
 template <bool ZERO>
 __device__ __forceinline__ bool t8_right_slow(uint32_t x, uint32_t b) {
   using W = RxBins<true>;
@@ -2054,34 +2020,11 @@ __device__ __forceinline__ void t8_stage(const KArgs& a, ACC (&acc)[KMAX], int t
       x[q] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
           static_cast<uintptr_t>(base[q] + 4u * nd[q]));
     }
-#if TI_T8_MASK
-    // lanes at a leaf skip the step's reads (exec-masked: they take no part
-    // in the banking of the pair read, whose random leaf-pair addresses made
-    // most of the bank conflicts); the stale pair is the leaf's own pair, so
-    // the select still returns the leaf word, for any bin (see above)
-    uint32_t b[ILP];
-    rx_u2_t pr[ILP];
-#pragma unroll
-    for (int q = 0; q < ILP; ++q) {
-      b[q] = 1u;
-      pr[q].x = x[q];
-      pr[q].y = x[q];
-    }
-#endif
     for (;;) {
       uint32_t all = x[0];
 #pragma unroll
       for (int q = 1; q < ILP; ++q) all &= x[q];
       if (__ballot((all & W::kLeaf) == 0u) == 0) break;   // every lane of every tree at a leaf
-#if TI_T8_MASK
-#pragma unroll
-      for (int q = 0; q < ILP; ++q) {
-        if ((x[q] & W::kLeaf) == 0u) {
-          b[q] = lds_u8((x[q] & W::kNodeMask) | lane_off);
-          pr[q] = lx_rec(base[q] + ((x[q] >> 24) << 3));
-        }
-      }
-#else
       uint32_t b[ILP];
       rx_u2_t pr[ILP];
 #pragma unroll
@@ -2089,7 +2032,6 @@ __device__ __forceinline__ void t8_stage(const KArgs& a, ACC (&acc)[KMAX], int t
         b[q] = lds_u8((x[q] & W::kNodeMask) | lane_off);
         pr[q] = lx_rec(base[q] + ((x[q] >> 24) << 3));
       }
-#endif
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
         if (!SLOW) {

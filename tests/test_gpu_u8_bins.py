@@ -237,6 +237,8 @@ def test_u8_vector_leaves_sklearn_classifier(monkeypatch):
     X = rng.integers(-2, 62, (3000, 12)).astype(np.float32)
     X[rng.random(X.shape) < 0.01] = np.nan
     want = est.predict_proba(X)
-    got = d8.predict(X, OUT_PREDICT)
+    got = d8.predict(X, OUT_MARGIN)                  # a classifier's margin: the mean proba
     np.testing.assert_array_equal(got.reshape(want.shape), want)
-    assert np.array_equal(got, d16.predict(X, OUT_PREDICT))
+    assert np.array_equal(got, d16.predict(X, OUT_MARGIN))
+    assert np.array_equal(d8.predict(X, OUT_PREDICT), est.predict(X).astype(np.float64))
+    assert np.array_equal(d8.predict(X, OUT_LEAF), d16.predict(X, OUT_LEAF))
