@@ -18,7 +18,9 @@ def test_c2_roofline_from_committed_pmc_pass():
     rf = bench.roofline(0.7226, 1_000_000, C2_INFO, PMC_C2)
     assert "error" not in rf, rf.get("error")
     assert rf["bound"] == "lds_array"
-    assert rf["frac"] == pytest.approx(0.683, abs=0.01)     # 281.2M / (256 x 1.6088M)
+    pmc = bench.load_pmc(PMC_C2)        # LDS-array cycles / (256 CUs x the pass's cycles)
+    want = pmc["lds_idx_active_per_launch"] / (256 * pmc["lds_pass_cycles_per_xcd"])
+    assert rf["frac"] == pytest.approx(want, rel=1e-12) and 0.5 < rf["frac"] < 0.9
     assert rf["achieved"] == pytest.approx(rf["frac"] * 2.4, rel=1e-9)
     assert rf["traffic"] and rf["traffic"] > rf["hbm_compulsory_bytes"]
     assert 0 < rf["lds_bank_conflict_frac"] < 0.5
