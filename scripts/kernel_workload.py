@@ -42,6 +42,8 @@ def main():
     p.add_argument("--workload", required=True)
     p.add_argument("--rows", type=int, default=1_000_000)
     p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--trees", type=int, default=0,
+                   help="c2 / c2_hist only: the first N trees (fixed cost vs per-tree cost)")
     p.add_argument("--x-buffers", type=int, default=1,
                    help="copies of the batch the launches rotate through (bench.py uses 3 for C2)")
     a = p.parse_args()
@@ -50,6 +52,12 @@ def main():
     from kfserving_amd.engine import DeviceForest
     from kfserving_amd.forest import OUT_PREDICT, TI_F32, TI_F64
     forest, F, dtype = forest_of(a.workload)
+    if a.trees and a.workload in ("c2", "c2_hist"):
+        from kfserving_amd.formats.xgboost_format import (forest_from_raw_trees,
+                                                          synthetic_complete_trees)
+        trees, ti = synthetic_complete_trees(bench.N_TREES, bench.DEPTH, F, seed=0,
+                                             max_bin=254 if a.workload == "c2_hist" else 0)
+        forest = forest_from_raw_trees(trees[:a.trees], ti[:a.trees], F, 0, 0.0, "binary:logistic")
     dev = DeviceForest(forest, [0])
     Xs = [bench.device_normal(a.rows, F, 3, "cuda:0", dtype)]
     Xs += [Xs[0].clone() for _ in range(max(0, a.x_buffers - 1))]
@@ -74,7 +82,7 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.steps
     info = dev.info()
-    print(json.dumps({"workload": a.workload, "rows": a.rows, "dtype": dtype,
+    print(json.dumps({"workload": a.workload, "rows": a.rows, "dtype": dtype, "trees": forest.n_trees,
                       "layout": bench.LAYOUT_NAMES.get(info["layout"]), "walk": info["walk"],
                       "bin_bits": info["bin_bits"], "tree_ilp": info["tree_ilp"],
                       "n_stages": info["n_stages"], "top_depth": info["top_depth"],
