@@ -2252,10 +2252,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
       // kFixStage]; the binning goes through the stage area, 4 NG columns at a
       // time.  NG = 1: 38,912 B, 4 workgroups (32 waves) per CU
       const int ng = std::min(2, std::max(1, env_int("TI_BHEAP_NG", 1)));
-      // TI_FIX_BINQ=8: the tile's binning searches 8 features at once through
-      // the 4-column stage area (stage_bins_q)
-      const bool q8 = ng == 1 && env_int("TI_FIX_BINQ", 4) == 8;
-      fn = ti::kernels_ff(10, f->K, true, false, bi.b16 != 0, q8 ? 3 : ng);
+      fn = ti::kernels_ff(10, f->K, true, false, bi.b16 != 0, ng);
       a.stage_trees = 4 * ng;
       a.bin_chunk = 4 * ng;
       a.stage_off = static_cast<int32_t>(ti::kFixStage);

@@ -656,88 +656,6 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
   return *flag != 0;
 }
 
-// stage_bins with more independent search chains than the temp area holds
-// columns: the Q features of a round are loaded CH columns at a time through
-// the same temp (barrier, coalesced copy, barrier, each lane reads its CH
-// values into registers), then searched together -- Q dependent-gather
-// chains per lane instead of CH, so a tile's binning waits on F / Q rounds
-// of H gathers instead of F / CH (the fixed walk: CH = 4 columns of 512 rows
-// in its 8 KB stage area, Q = 8).  Same bins, same NaN flag.
-template <typename XT, bool B16, int Q, int CH>
-__device__ __forceinline__ bool stage_bins_q(volatile int* flag, XT* temp, const KArgs& a,
-                                             int64_t row0, int R, int tid) {
-  using BT = BinTraits<B16>;
-  constexpr int P = BT::P;
-  static_assert(Q % CH == 0 && Q % P == 0, "rounds of whole chunks and words");
-  const XT* X = static_cast<const XT*>(a.X);
-  const int F = a.n_features;
-  const int C = a.n_cols;
-  const int64_t left_rows = a.n_rows - row0;
-  const int rows_here = left_rows < R ? (int)left_rows : R;
-  const bool vec_ok = ((reinterpret_cast<uintptr_t>(X) | (uintptr_t)(a.row_stride * sizeof(XT))) & 15) == 0;
-  constexpr int V = 16 / sizeof(XT);   // elements per 16-byte load
-  bool has_nan = false;
-  if (tid == 0) *flag = 0;
-  for (int f0 = 0; f0 < F; f0 += Q) {
-    XT x[Q];
-#pragma unroll
-    for (int s = 0; s < Q; s += CH) {
-      const int fs = f0 + s;
-      const int kc = fs >= F ? 0 : ((F - fs) < CH ? (F - fs) : CH);
-      __syncthreads();   // temp is free (its previous chunk is in registers)
-      const bool vec = vec_ok && (fs % V) == 0 && (kc % V) == 0 && fs + kc <= C && kc > 0;
-      const uint32_t n = (uint32_t)rows_here * (uint32_t)kc;
-      const uint32_t ukc = (uint32_t)(kc > 0 ? kc : 1);
-      if (vec) {
-        typedef XT xv_t __attribute__((ext_vector_type(V)));
-        const uint32_t kv = ukc / V;
-        const uint32_t nv = (uint32_t)rows_here * kv;
-        for (uint32_t e = tid; e < nv; e += R) {
-          const uint32_t r = e / kv;
-          const uint32_t cv = e - r * kv;
-          const xv_t v = *reinterpret_cast<const xv_t*>(X + (row0 + r) * a.row_stride + fs + cv * V);
-#pragma unroll
-          for (int j = 0; j < V; ++j) temp[(cv * V + j) * R + r] = zero_map(v[j], a.lgb_zero_map);
-        }
-      }
-      for (uint32_t e = vec ? n : tid; e < n; e += R) {
-        const uint32_t r = e / ukc;
-        const uint32_t c = e - r * ukc;
-        const int f = fs + (int)c;
-        const XT v = f < C ? X[(row0 + r) * a.row_stride + f] : nan_value<XT>();
-        temp[c * R + r] = zero_map(v, a.lgb_zero_map);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < CH; ++j) x[s + j] = j < kc ? temp[j * R + tid] : nan_value<XT>();
-    }
-    uint32_t b[Q];
-    rank_search<XT, Q>(a, x, f0, b);
-    uint32_t w[Q / P];
-#pragma unroll
-    for (int j = 0; j < Q / P; ++j) w[j] = 0u;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const bool nan = x[q] != x[q];
-      has_nan |= nan && (f0 + q < F);
-      w[q / P] |= (nan ? BT::kNan : b[q]) << ((q % P) * (32 / P));
-    }
-#pragma unroll
-    for (int j = 0; j < Q / P; ++j) {
-      const int word = f0 / P + j;
-      if (f0 + j * P < F) {
-        __attribute__((address_space(3))) uint32_t* dst =
-            reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-                static_cast<uintptr_t>((uint32_t)(word * R + tid) * 4u));
-        *dst = w[j];
-      }
-    }
-  }
-  if (has_nan && tid < rows_here) *flag = 1;
-  __syncthreads();
-  return *flag != 0;
-}
-
 // Walk one LDS stage of binned complete trees.  A tree record is 2^D u32
 // entries (1-based heap: node i has children 2i and 2i+1; entry 0 unused),
 // then 2^D * leaf_width leaves (ACC).  At each level a lane issues the bin
@@ -1054,7 +972,7 @@ __device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0,
   }
 }
 
-template <typename XT, int KMAX, bool B16, int NG, int QB = 4 * NG>
+template <typename XT, int KMAX, bool B16, int NG>
 __global__ void __launch_bounds__(512) bheap_fix_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int R = kFixRows;
@@ -1079,11 +997,8 @@ __global__ void __launch_bounds__(512) bheap_fix_kernel(const KArgs a) {
     const int i = tid + u * R;
     pf[u] = src[i < n16_all ? i : n16_all - 1];
   }
-  const bool tile_nan =
-      QB == 4 * NG ? stage_bins<XT, B16, 4 * NG>(flag, reinterpret_cast<XT*>(smem + kFixStage), a,
-                                                 row0, R, tid)
-                   : stage_bins_q<XT, B16, QB, 4 * NG>(flag, reinterpret_cast<XT*>(smem + kFixStage),
-                                                       a, row0, R, tid);
+  const bool tile_nan = stage_bins<XT, B16, 4 * NG>(
+      flag, reinterpret_cast<XT*>(smem + kFixStage), a, row0, R, tid);
   float acc[KMAX];
   init_acc(acc, a);
   u32x4 top[4 * NG] = {};
