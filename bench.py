@@ -547,10 +547,17 @@ def c2_hist_forest():
             "XGBoost binary:logistic, 500 x depth 8, thresholds on 253 quantile bin bounds")
 
 
+_C3_CACHE = []
+
+
 def c3_forest():
-    from kfserving_amd.formats import lightgbm_format as lf
-    return _lgb_forest(lf.synthetic_leafwise_trees(1000, 255, 100, seed=1),
-                       "LightGBM text v3, seeded leaf-wise generator (i.i.d. N(0,1) thresholds)")
+    """The C3 forest (built once: c3 and c3_f64 share it)."""
+    if not _C3_CACHE:
+        from kfserving_amd.formats import lightgbm_format as lf
+        _C3_CACHE.append(_lgb_forest(lf.synthetic_leafwise_trees(1000, 255, 100, seed=1),
+                                     "LightGBM text v3, seeded leaf-wise generator "
+                                     "(i.i.d. N(0,1) thresholds)"))
+    return _C3_CACHE[0]
 
 
 def c3_maxbin_forest():
