@@ -553,3 +553,26 @@ def test_sklearn_gradient_boosting_gpu_bit_exact(tmp_path):
     assert got == est.predict(Xt[:64]).tolist()
     with pytest.raises(Exception, match="NaN"):
         model.predict({"instances": [[float("nan")] * 7]})
+
+
+@pytest.mark.parametrize("layout", ["rexplicit", "lexplicit", "hexplicit", "texplicit"])
+def test_cover_order_changes_layout_only(golden, layout, monkeypatch):
+    """Hot-nodes-first slots (cover_order / leaf_order) against breadth-first
+    slots (TI_COVER_ORDER=0) and a forest without covers: probabilities and
+    leaf ids identical on every record layout (vector leaves through the
+    leaf tables, whose numbering follows the slot order)."""
+    fc = load_tree_arrays(os.path.join(golden, "sk_rf_clf_model.npz"))
+    gc = np.load(os.path.join(golden, "sk_rf_clf.npz"))
+    outs = []
+    for setting in ("1", "0", "none"):
+        monkeypatch.setenv("TI_COVER_ORDER", "0" if setting == "0" else "1")
+        f = fc
+        if setting == "none":
+            import copy
+            f = copy.copy(fc)
+            f.cover = None
+        dev = _dev_with_layout(f, layout)
+        assert dev.info()["layout"] == LAYOUT_ID[layout]
+        outs.append((dev.predict(gc["X"], OUT_MARGIN), dev.predict(gc["X"], OUT_LEAF)))
+    for m, leaf in outs:
+        assert np.array_equal(m, gc["predict_proba"]) and np.array_equal(leaf, gc["apply"])
