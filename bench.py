@@ -13,7 +13,7 @@ Also reported (rank 0):
                   the busiest of VALU issue, the LDS array and the TD in the
                   committed rocprofv3 PMC pass of the same kernel
                   (profiles/r4c_c2_pmc.json), priced on that pass's own cycles
-                  (GRBM_GUI_ACTIVE per XCD): the LDS array, ~0.74.  `valu`
+                  (GRBM_GUI_ACTIVE per XCD): the LDS array, ~0.67.  `valu`
                   keeps the VALU view: achieved = VALU wave-instructions per
                   launch / the kernel's average duration from HIP events on
                   the launch stream; peak = 1,024 SIMDs x 2.4 GHz / 2 cycles
