@@ -2247,30 +2247,24 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
                                                         static_cast<size_t>(f->F + 7) & ~size_t(7)));
     lds = fixed + ar;
     KernelFn fn = select_bheap(xdt, f->accum, f->K, bi.b16 != 0, pf);
-    int block = R;   // rows (threads) of a workgroup
     if (bheap_fixed(f, xdt, kind)) {
       // fixed layout (bheap_fix_kernel): [bins][flag][NG groups of 4 trees at
       // kFixStage]; the binning goes through the stage area, 4 NG columns at a
-      // time.  NG = 1: 38,912 B, 4 workgroups (32 waves) per CU.
-      // TI_FIX_HALVES=2: 1,024-row tiles of two 512-row images (FixLayout<2>):
-      // 79,872 B, 2 workgroups (32 waves) per CU
+      // time.  NG = 1: 38,912 B, 4 workgroups (32 waves) per CU
       const int ng = std::min(2, std::max(1, env_int("TI_BHEAP_NG", 1)));
-      const bool halves = ng == 1 && env_int("TI_FIX_HALVES", 1) == 2;
-      fn = ti::kernels_ff(10, f->K, true, false, bi.b16 != 0, halves ? 3 : ng);
+      fn = ti::kernels_ff(10, f->K, true, false, bi.b16 != 0, ng);
       a.stage_trees = 4 * ng;
       a.bin_chunk = 4 * ng;
-      a.stage_off = static_cast<int32_t>(halves ? ti::FixLayout<2>::kStage : ti::kFixStage);
+      a.stage_off = static_cast<int32_t>(ti::kFixStage);
       if (fix_perm) a.trees = d.bh_fix_img;   // same walk, hot pair slots first
-      lds = halves ? ti::FixLayout<2>::kStage + ti::FixLayout<2>::kTemp
-                   : ti::kFixStage + static_cast<size_t>(4 * ng) * ti::kFixTree;
-      block = halves ? 2 * ti::kFixRows : ti::kFixRows;
+      lds = ti::kFixStage + static_cast<size_t>(4 * ng) * ti::kFixTree;
     }
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
-    const int64_t grid = (rows + block - 1) / block;
+    const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    occ_note(fn, block, lds);
-  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(block), lds, stream, a);
+    occ_note(fn, R, lds);
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
   } else if (f->layout == 6) {

@@ -75,12 +75,9 @@ KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
     return rexplicit_predict_kernel<XT, ACC, KMAX, false, 4>;
   }
   if (layout == 10) {   // binned heap, fixed layout: float X, float sums; pf carries NG
-                        // (1, 2), or 3: NG 1 on two-half 1,024-row tiles
     if constexpr (sizeof(XT) == 4 && sizeof(ACC) == 4) {
-      if (b16) return pf == 3 ? bheap_fix_kernel<XT, KMAX, true, 1, 2>
-                    : pf >= 2 ? bheap_fix_kernel<XT, KMAX, true, 2> : bheap_fix_kernel<XT, KMAX, true, 1>;
-      return pf == 3 ? bheap_fix_kernel<XT, KMAX, false, 1, 2>
-             : pf >= 2 ? bheap_fix_kernel<XT, KMAX, false, 2> : bheap_fix_kernel<XT, KMAX, false, 1>;
+      if (b16) return pf >= 2 ? bheap_fix_kernel<XT, KMAX, true, 2> : bheap_fix_kernel<XT, KMAX, true, 1>;
+      return pf >= 2 ? bheap_fix_kernel<XT, KMAX, false, 2> : bheap_fix_kernel<XT, KMAX, false, 1>;
     }
     return nullptr;
   }

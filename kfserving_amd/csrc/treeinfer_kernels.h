@@ -581,10 +581,7 @@ __device__ __forceinline__ void rank_search(const KArgs& a, const XT (&x)[Q], in
 // values (rank_search), Q features at once for Q independent load chains.
 // Returns (uniformly) whether a live row of the tile holds a NaN.  Ends in a
 // barrier.
-// IMG_R > 0 (the fixed walk's two-half tiles): the bin image is R / IMG_R
-// images of IMG_R rows, half h at LDS byte h << 15, so a lane's column is
-// (tid % IMG_R) * 4 | (tid / IMG_R) << 15 (fix_lane_off).
-template <typename XT, bool B16, int Q = TI_BIN_Q, int IMG_R = 0>
+template <typename XT, bool B16, int Q = TI_BIN_Q>
 __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const KArgs& a,
                                            int64_t row0, int R, int tid) {
   using BT = BinTraits<B16>;
@@ -646,13 +643,9 @@ __device__ __forceinline__ bool stage_bins(volatile int* flag, XT* temp, const K
       for (int j = 0; j < Q / P; ++j) {
         const int word = (f0 + c) / P + j;
         if (c + j * P < kc) {
-          const uint32_t at =
-              IMG_R > 0 ? (uint32_t)(word * IMG_R * 4) + (((uint32_t)tid % IMG_R) * 4u |
-                                                          ((uint32_t)tid / IMG_R) << 15)
-                        : (uint32_t)(word * R + tid) * 4u;
           __attribute__((address_space(3))) uint32_t* dst =
               reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-                  static_cast<uintptr_t>(at));
+                  static_cast<uintptr_t>((uint32_t)(word * R + tid) * 4u));
           *dst = w[j];
         }
       }
@@ -876,21 +869,6 @@ constexpr uint32_t kFixFlag = 28672u;
 constexpr uint32_t kFixStage = 30720u;
 constexpr int kFixRows = 512;
 constexpr int kFixTree = 2048;   // 256 node words + 256 float leaves
-// Two-half tiles (H = 2, TI_FIX_HALVES=2): 1,024 rows a workgroup (16 waves),
-// the bin image as two 512-row images at LDS 0 and 32 KB (the node words'
-// bin offsets stay those of a 512-row image; the half is the lane's bit 15),
-// flag and stage after them, the binning's X columns through 16 KB from the
-// stage on.  Each workgroup stages the forest once for 1,024 rows, not 512.
-template <int H> struct FixLayout {
-  static constexpr uint32_t kFlag = H == 1 ? kFixFlag : 61440u;
-  static constexpr uint32_t kStage = H == 1 ? kFixStage : 63488u;
-  static constexpr uint32_t kTemp = H == 1 ? 8192u : 16384u;   // binning temp bytes
-};
-template <int H>
-__device__ __forceinline__ uint32_t fix_lane_off(int tid) {
-  return H == 1 ? (uint32_t)tid * 4u
-                : (((uint32_t)tid & (kFixRows - 1)) * 4u) | (((uint32_t)tid / kFixRows) << 15);
-}
 
 __device__ __forceinline__ uint2 lds_u2c(uint32_t byte_addr) {
   const uint64_t v = *reinterpret_cast<const __attribute__((address_space(3))) uint64_t*>(
@@ -941,7 +919,7 @@ __device__ __forceinline__ void fix_step(uint32_t& nd, uint32_t b, uint2 pr) {
         : "vcc", "scc");
   }
 }
-template <int KMAX, bool B16, bool CHECK_NAN, int NG, uint32_t STAGE = kFixStage>
+template <int KMAX, bool B16, bool CHECK_NAN, int NG>
 __device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0, float (&acc)[KMAX],
                                                 uint32_t lane_off, const u32x4 (&top)[4 * NG]) {
   const uint32_t bmask = a.bin_mask;
@@ -968,7 +946,7 @@ __device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0,
 #else
     (void)top;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) nd[q] = lds_u32(STAGE + (uint32_t)((g * 4 + q) * kFixTree) + 4u);
+    for (int q = 0; q < 4; ++q) nd[q] = lds_u32(kFixStage + (uint32_t)((g * 4 + q) * kFixTree) + 4u);
     constexpr int l_first = 0;
 #endif
 #pragma unroll
@@ -978,7 +956,7 @@ __device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0,
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         b[q] = lds_bin<B16>((nd[q] & bmask) | lane_off);
-        pr[q] = lds_u2c((nd[q] & kBNodePairMask) + (STAGE + (uint32_t)((g * 4 + q) * kFixTree)));
+        pr[q] = lds_u2c((nd[q] & kBNodePairMask) + (kFixStage + (uint32_t)((g * 4 + q) * kFixTree)));
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) fix_step<B16, CHECK_NAN>(nd[q], b[q], pr[q]);
@@ -994,37 +972,33 @@ __device__ __forceinline__ void bheap_fix_stage(const KArgs& a, int cnt, int t0,
   }
 }
 
-template <typename XT, int KMAX, bool B16, int NG, int H = 1>
-__global__ void __launch_bounds__(512 * H) bheap_fix_kernel(const KArgs a) {
+template <typename XT, int KMAX, bool B16, int NG>
+__global__ void __launch_bounds__(512) bheap_fix_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using L = FixLayout<H>;
-  constexpr int R = kFixRows * H;
+  constexpr int R = kFixRows;
   constexpr int S = 4 * NG;   // trees per stage
   const int tid = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * R;
   const int64_t row = row0 + tid;
   const bool live = row < a.n_rows;
-  volatile int* flag = reinterpret_cast<volatile int*>(smem + L::kFlag);
-  u32x4* stage = reinterpret_cast<u32x4*>(smem + L::kStage);
-  const uint32_t lane_off = fix_lane_off<H>(tid);
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + kFixFlag);
+  u32x4* stage = reinterpret_cast<u32x4*>(smem + kFixStage);
+  const uint32_t lane_off = (uint32_t)tid * 4u;
   const int T = a.n_trees;
   constexpr int n16 = S * kFixTree / 16;   // 16-byte words per stage: NG per thread
-  static_assert(n16 == NG * kFixRows, "one 16-byte word per thread of a 512-row half and group");
+  static_assert(n16 == NG * R, "one 16-byte word per thread and group");
   const u32x4* src = reinterpret_cast<const u32x4*>(a.trees);
   const int n16_all = (int)(((int64_t)T * kFixTree) >> 4);
   // first stage in flight while the tile is binned (a clamped lane re-reads
   // the forest's last word; its stage slot then holds a word no tree reads)
-  // a stage is NG words of 16 B per thread of a 512-row half: with two
-  // halves, the first half's threads copy it (ct: copying thread)
-  const bool ct = H == 1 || tid < kFixRows;
   u32x4 pf[NG];
 #pragma unroll
   for (int u = 0; u < NG; ++u) {
-    const int i = tid + u * kFixRows;
-    pf[u] = ct ? src[i < n16_all ? i : n16_all - 1] : u32x4{0u, 0u, 0u, 0u};
+    const int i = tid + u * R;
+    pf[u] = src[i < n16_all ? i : n16_all - 1];
   }
-  const bool tile_nan = stage_bins<XT, B16, 4 * NG, H == 1 ? 0 : kFixRows>(
-      flag, reinterpret_cast<XT*>(smem + L::kStage), a, row0, R, tid);
+  const bool tile_nan = stage_bins<XT, B16, 4 * NG>(
+      flag, reinterpret_cast<XT*>(smem + kFixStage), a, row0, R, tid);
   float acc[KMAX];
   init_acc(acc, a);
   u32x4 top[4 * NG] = {};
@@ -1034,23 +1008,21 @@ __global__ void __launch_bounds__(512 * H) bheap_fix_kernel(const KArgs a) {
 #if TI_FIX_SROOT
     fix_tops<NG>(a, t0, top);
 #endif
-    if (ct) {
 #pragma unroll
-      for (int u = 0; u < NG; ++u) stage[tid + u * kFixRows] = pf[u];
-    }
+    for (int u = 0; u < NG; ++u) stage[tid + u * R] = pf[u];
     __syncthreads();
-    if (ct) {
+    {
       const int base = (t0 + S) * (kFixTree / 16);
 #pragma unroll
       for (int u = 0; u < NG; ++u) {
-        const int i = base + tid + u * kFixRows;
+        const int i = base + tid + u * R;
         pf[u] = src[i < n16_all ? i : n16_all - 1];
       }
     }
     if (tile_nan)
-      bheap_fix_stage<KMAX, B16, true, NG, L::kStage>(a, cnt, t0, acc, lane_off, top);
+      bheap_fix_stage<KMAX, B16, true, NG>(a, cnt, t0, acc, lane_off, top);
     else
-      bheap_fix_stage<KMAX, B16, false, NG, L::kStage>(a, cnt, t0, acc, lane_off, top);
+      bheap_fix_stage<KMAX, B16, false, NG>(a, cnt, t0, acc, lane_off, top);
   }
   if (!live) return;
   finish_row<float, KMAX>(acc, a, row);

@@ -164,7 +164,7 @@ def _with_env(env, fn):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("ng", ["1", "2", "1h2"])
+@pytest.mark.parametrize("ng", ["1", "2"])
 @pytest.mark.parametrize("quantize", [16, None], ids=["u8", "u16"])
 def test_bheap_fixed_walk(quantize, ng):
     """The fixed-layout walk (bheap_fix_kernel: compile-time LDS addresses, the
@@ -183,8 +183,7 @@ def test_bheap_fixed_walk(quantize, ng):
             v[:] = np.round(v * quantize) / quantize
     forest = xf.forest_from_raw_trees(trees, ti, 28, 0, 0.5, "binary:logistic")
     ref = xgb_ref.from_raw_trees(trees, ti, 28, 0, 0.5, "binary:logistic")
-    # "1h2": one stage group on two-half 1,024-row tiles (FixLayout<2>)
-    env = {"TI_BHEAP_NG": ng[0], "TI_FIX_HALVES": "2" if ng.endswith("h2") else "1"}
+    env = {"TI_BHEAP_NG": ng}
     dev = _with_env(env, lambda: DeviceForest(forest, [0]))
     inf = dev.info()
     assert inf["layout"] == BHEAP and inf["walk"] == 2 and inf["depth"] == 8
