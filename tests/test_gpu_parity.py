@@ -312,6 +312,21 @@ def test_c2_full_size_matches_c_port():
     np.testing.assert_allclose(prob, 1.0 / (1.0 + np.exp(-want.astype(np.float64))), rtol=RTOL)
 
 
+def test_c2_hist_full_size_matches_c_port():
+    """The bench's `c2_hist` key at full size: C2's trees with thresholds on
+    253 quantile bin bounds (u8 bins, the fixed walk's u8 instance and its
+    cover-permuted image), 1M rows with 1 % NaN: every margin bit-exact
+    against the C restatement of xgboost 0.82."""
+    trees, ti = xf.synthetic_complete_trees(500, 8, 28, seed=0, max_bin=254)
+    dev = DeviceForest(xf.forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic"), [0])
+    info = dev.info()
+    assert info["layout"] == 3 and info["bin_bits"] == 8 and info["walk"] == 2
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((1_000_000, 28), dtype=np.float32)
+    X[rng.random(X.shape, dtype=np.float32) < 0.01] = np.nan
+    assert np.array_equal(dev.predict(X, OUT_MARGIN), port.xgb_predict(trees, ti, 1, 0.0, 28, X)[:, 0])
+
+
 def test_leafwise_lgb_full_property():
     """Config C3 shape (1000 trees x 255 leaves, 100 features) on 200k rows:
     raw scores bit-exact against the C restatement of lightgbm 2.3.1."""
