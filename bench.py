@@ -136,6 +136,9 @@ def parse_args(argv=None):
     p.add_argument("--rows4", type=int, default=10_000_000)
     p.add_argument("--config-steps", type=int, default=2)
     p.add_argument("--pmc-json", default=os.path.join(ROOT, PMC_PASSES["c2"]))
+    p.add_argument("--streams", type=int, default=2,
+                   help="launch streams the headline's steps rotate over (batches in flight); "
+                        "the roofline prices the one-stream launch duration")
     p.add_argument("--x-buffers", type=int, default=3,
                    help="copies of the batch the timed steps rotate through (3 x 112 MB "
                         "exceeds the 256 MB Infinity Cache)")
@@ -191,16 +194,22 @@ def barrier_sync(dev_sync):
     dev_sync()
 
 
-def timed_steps(step, steps, dev_sync, events=None):
+def timed_steps(step, steps, dev_sync, events=None, fork=None, join=None):
     """K steps bracketed by barrier + device sync on both sides; returns the
     wall time and (with `events` = (start, end) timing events recorded on the
-    launch stream) the event time per step in ms."""
+    launch stream) the event time per step in ms.  fork / join (--streams > 1)
+    make the other launch streams wait for the start event and the launch
+    stream wait for them before the end event."""
     barrier_sync(dev_sync)
     t0 = time.perf_counter()
     if events:
         events[0].record()
+    if fork:
+        fork()
     for _ in range(steps):
         step()
+    if join:
+        join()
     if events:
         events[1].record()
     barrier_sync(dev_sync)
@@ -747,21 +756,56 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
     out = torch.empty(rows, dtype=torch.float32, device=device)
     sh = torch.cuda.current_stream().cuda_stream if device != "cpu" else 0
     it = [0]
+    # --streams S > 1: consecutive steps (independent batches) go round-robin
+    # over S streams, each with its own output, as batches in flight do
+    n_str = max(1, args.streams) if device != "cpu" else 1
+    strs = [None] + [torch.cuda.Stream(device=device) for _ in range(n_str - 1)]
+    outs = [out] + [torch.empty_like(out) for _ in range(n_str - 1)]
 
-    def step():
+    def launch(k):
         Xi = Xs[it[0] % len(Xs)]
         it[0] += 1
         dev.predict_device(Xi.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
-                           out.data_ptr(), rows, slot=0, stream=sh)
+                           outs[k].data_ptr(), rows, slot=0,
+                           stream=sh if k == 0 else strs[k].cuda_stream)
 
+    def step1():   # one stream: each launch alone on the chip
+        launch(0)
+
+    def step():    # --streams S: batch i on stream i mod S
+        launch(it[0] % n_str)
+
+    def fork():
+        for st in strs[1:]:
+            st.wait_stream(torch.cuda.current_stream())
+
+    def join():
+        for st in strs[1:]:
+            torch.cuda.current_stream().wait_stream(st)
+
+    def events():
+        return ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                if device != "cpu" else None)
+
+    # K steps on one stream: the kernel's own launch duration (events on the
+    # stream it runs on), which the roofline and the rocprof summary price
     for _ in range(args.warmup):
-        step()
-    ev = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          if device != "cpu" else None)
-    wall, kernel_ms = timed_steps(step, args.steps, dev_sync, ev)
+        step1()
+    wall1, kernel_ms = timed_steps(step1, args.steps, dev_sync, events())
     if kernel_ms is None:
-        kernel_ms = wall / args.steps * 1e3
-    wall = max_over_ranks(wall, device)
+        kernel_ms = wall1 / args.steps * 1e3
+    wall1 = max_over_ranks(wall1, device)
+    wall = wall1
+    if n_str > 1:
+        # the headline: the same K steps with S batches in flight, so one
+        # batch's binning and tail overlap the previous batch's walk
+        for _ in range(args.warmup):
+            step()
+        wall, _ = timed_steps(step, args.steps, dev_sync, events(), fork, join)
+        wall = max_over_ranks(wall, device)
+    # every X buffer is a copy of one batch: each stream's last output must be
+    # the same rows, bit for bit (no batch in flight was skipped or cut short)
+    outputs_identical = all(bool(torch.equal(outs[0], o)) for o in outs[1:])
     value = rows * world * args.steps / wall
 
     # the serving-latency leg runs right after the headline, before the legs
@@ -856,7 +900,12 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
                                    "500 trees depth 8, 1M-row batch per GPU",
                        "rows_per_gpu": rows, "trees": N_TREES, "depth": DEPTH,
                        "features": N_FEAT, "layout": LAYOUT_NAMES.get(info["layout"]),
-                       "parallelism": f"rows sharded x{world}", "x_buffers": len(Xs)},
+                       "parallelism": f"rows sharded x{world}", "x_buffers": len(Xs),
+                       "streams": n_str},
+            "single_stream": {"ms_per_step": wall1 / args.steps * 1e3,
+                              "value": rows * world * args.steps / wall1,
+                              "kernel_ms": kernel_ms},
+            "streams_outputs_identical": outputs_identical,
             "roofline": roofline(kernel_ms, rows, info, args.pmc_json),
             "cpu_baseline": cpu,
             "batched_latency": latency,

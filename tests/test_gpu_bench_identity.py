@@ -35,3 +35,19 @@ def test_config_launch_matches_pmc_pass(key):
     info = _info(forest)
     pmc = bench.load_pmc(bench.pmc_path(key))
     assert bench.pmc_mismatch(pmc, key, None, info) is None, info
+
+
+def test_headline_two_streams_same_outputs():
+    """The headline's batches in flight (--streams 2) compute every row: each
+    stream's output equals the others' bit for bit, the one-stream kernel time
+    is reported beside, and value = rows x steps / the multi-stream wall."""
+    args = bench.parse_args(["--steps", "6", "--warmup", "2", "--rows", "262144", "--configs", "",
+                             "--no-cpu-baseline", "--latency-qps", "0", "--host-rows", "0",
+                             "--nan-variant", "0", "--streams", "2"])
+    line = bench.run(args)
+    assert line["config"]["streams"] == 2
+    assert line["streams_outputs_identical"] is True
+    ss = line["single_stream"]
+    assert ss["kernel_ms"] > 0 and ss["ms_per_step"] > 0
+    assert abs(line["value"] - 262144 * 6 / (line["ms_per_step"] * 6e-3)) < 1e-6 * line["value"]
+    assert line["roofline"]["kernel_ms"] == ss["kernel_ms"]
