@@ -46,6 +46,8 @@ def main():
                    help="c2 / c2_hist only: the first N trees (fixed cost vs per-tree cost)")
     p.add_argument("--x-buffers", type=int, default=1,
                    help="copies of the batch the launches rotate through (bench.py uses 3 for C2)")
+    p.add_argument("--streams", type=int, default=1,
+                   help="launch streams the steps rotate over (batches in flight, as bench.py --streams)")
     a = p.parse_args()
     import torch
     import bench
@@ -63,21 +65,30 @@ def main():
     Xs += [Xs[0].clone() for _ in range(max(0, a.x_buffers - 1))]
     it = [0]
     xdt = TI_F64 if dtype == "float64" else TI_F32
-    out = torch.empty(a.rows * forest.output_width(OUT_PREDICT),
-                      dtype=torch.float64 if forest.accum_dtype else torch.float32, device="cuda")
-    sh = torch.cuda.current_stream().cuda_stream
+    S = max(1, a.streams)
+    outs = [torch.empty(a.rows * forest.output_width(OUT_PREDICT),
+                        dtype=torch.float64 if forest.accum_dtype else torch.float32, device="cuda")
+            for _ in range(S)]
+    cur = torch.cuda.current_stream()
+    strs = [cur] + [torch.cuda.Stream() for _ in range(S - 1)]
 
     def step():
         X = Xs[it[0] % len(Xs)]
+        k = it[0] % S
         it[0] += 1
-        dev.predict_device(X.data_ptr(), xdt, a.rows, F, F, OUT_PREDICT, out.data_ptr(),
-                           out.numel(), stream=sh)
-    step()
+        dev.predict_device(X.data_ptr(), xdt, a.rows, F, F, OUT_PREDICT, outs[k].data_ptr(),
+                           outs[k].numel(), stream=strs[k].cuda_stream)
+    for _ in range(S):
+        step()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
+    for st in strs[1:]:
+        st.wait_stream(cur)
     for _ in range(a.steps):
         step()
+    for st in strs[1:]:
+        cur.wait_stream(st)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.steps
@@ -86,7 +97,7 @@ def main():
                       "layout": bench.LAYOUT_NAMES.get(info["layout"]), "walk": info["walk"],
                       "bin_bits": info["bin_bits"], "tree_ilp": info["tree_ilp"],
                       "n_stages": info["n_stages"], "top_depth": info["top_depth"],
-                      "bottom": info["bottom"], "kernel_ms": ms,
+                      "bottom": info["bottom"], "streams": S, "kernel_ms": ms,
                       "rows_per_s": a.rows / (ms * 1e-3)}), flush=True)
     dev.close()
 
