@@ -79,6 +79,9 @@ def test_bench_rank_path_two_ranks():
     # the max over ranks: rank 1's 5 x 20 ms dominates
     assert line["ms_per_step"] >= 20.0
     assert abs(line["value"] - 4096 * 2 * 5 / (line["ms_per_step"] * 5e-3)) < 1e-6 * line["value"]
+    # no GPU: one stream, and the one-stream region is the headline's
+    assert line["config"]["streams"] == 1 and line["streams_outputs_identical"] is True
+    assert line["single_stream"]["value"] == line["value"]
     # C3: strong scaling, 500 rows per rank, 1 untimed + 2 timed steps
     assert calls0[1] == [(500, 100)] * 3 and calls1[1] == [(500, 100)] * 3
     c3 = line["c3"]
@@ -109,3 +112,11 @@ def test_bench_cli_gpus_n_starts_n_ranks():
     assert line["ms_per_step"] >= 20.0                    # rank 1's 20 ms steps dominate
     want = 2048 * 2 * 5 / (line["ms_per_step"] * 5e-3)
     assert abs(line["value"] - want) < 1e-6 * want
+
+
+def test_headline_defaults_two_streams():
+    """The headline keeps two batches in flight by default (DESIGN.md section
+    4); without a GPU there is one stream and the two timings coincide."""
+    import bench
+    assert bench.parse_args([]).streams == 2
+    assert bench.parse_args(["--streams", "1"]).streams == 1
