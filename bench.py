@@ -218,16 +218,65 @@ def timed_steps(step, steps, dev_sync, events=None, fork=None, join=None):
     return wall, ev_ms
 
 
+def streams_match(dev, Xs, outs, last_x, rows, sh, dev_sync, on_device=True):
+    """Each stream's last output equals a one-stream predict of the batch
+    that launch read (bit for bit).  None without a device (the CPU stand-in
+    engine writes no outputs)."""
+    import torch
+    from kfserving_amd.forest import OUT_PREDICT, TI_F32
+    if not on_device:
+        return None
+    dev_sync()
+    ok = True
+    for k, o in enumerate(outs):
+        if last_x[k] is None:
+            continue
+        ref = torch.empty_like(o)
+        Xi = Xs[last_x[k]]
+        dev.predict_device(Xi.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
+                           ref.data_ptr(), rows, slot=0, stream=sh)
+        dev_sync()
+        ok = ok and bool(torch.equal(ref, o))
+    return ok
+
+
+def batch_latency_events(launch, n_str, strs, steps, dev_sync):
+    """Untimed pass after the headline: the same round-robin launches with a
+    start and an end event around each on its own stream, so a batch's
+    launch-to-completion time beside the other stream's batch is measured
+    (the headline's own region carries no per-launch events)."""
+    import torch
+    cur = torch.cuda.current_stream()
+    dev_sync()
+    for st in strs[1:]:
+        st.wait_stream(cur)
+    evs = []
+    for i in range(steps):
+        k = i % n_str
+        s = cur if k == 0 else strs[k]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        launch(k)
+        e1.record(s)
+        evs.append((e0, e1))
+    dev_sync()
+    per = [a.elapsed_time(b) for a, b in evs]
+    return {"batch_ms_mean": float(np.mean(per)), "batch_ms_max": float(np.max(per)),
+            "batches": len(per),
+            "basis": "start/end HIP events around each launch on its own stream, "
+                     "round-robin over the streams as in the headline (untimed pass)"}
+
+
 def cpu_baseline(trees, ti, X_host, target_s):
     from oracle import port
-    n_thr = port.num_threads()
+    n_thr = baseline_threads()
     probe = min(20_000, X_host.shape[0])
     t0 = time.perf_counter()
-    port.xgb_predict(trees, ti, 1, 0.0, N_FEAT, X_host[:probe], sigmoid=True)
+    port.xgb_predict(trees, ti, 1, 0.0, N_FEAT, X_host[:probe], sigmoid=True, nthread=n_thr)
     rate = probe / max(time.perf_counter() - t0, 1e-9)
     n = int(min(X_host.shape[0], max(probe, rate * target_s)))
     t0 = time.perf_counter()
-    port.xgb_predict(trees, ti, 1, 0.0, N_FEAT, X_host[:n], sigmoid=True)
+    port.xgb_predict(trees, ti, 1, 0.0, N_FEAT, X_host[:n], sigmoid=True, nthread=n_thr)
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "rows/s", "cores": n_thr, "kind": "port",
             "sample": f"{n} rows of the same 1M x 28 batch, oracle/c/tree_port.c "
@@ -337,6 +386,40 @@ def roofline(kernel_ms: float, rows: int, info: dict, pmc_path: str):
 
 
 CUS = 256
+B_VISIT = 8 * N_TREES * DEPTH + 4 * N_FEAT + 4   # SURVEY.md 8(d)'s per-row visit bytes
+
+
+def headline_roofline(kernel_ms, rows, info, pmc_path, step_s, two_stream, n_str):
+    """roofline() of the one-stream launch, plus what the headline's own
+    region did: `two_stream` prices the PMC pass's LDS-array cycles per batch
+    on the two-stream step time (256 CUs x 2.4 GHz x ms_per_step) and carries
+    the per-batch launch-to-completion time measured with events; `b_visit_*`
+    is SURVEY.md 8(d)'s visit-byte model, whose nodes are LDS-resident, so
+    its fraction of HBM peak is not a bound (it exceeds 1)."""
+    out = roofline(kernel_ms, rows, info, pmc_path)
+    bv = B_VISIT * rows / (kernel_ms * 1e-3)
+    out["b_visit_bytes_per_row"] = B_VISIT
+    out["b_visit_GBps"] = bv / 1e9
+    out["b_visit_frac"] = bv / HBM_PEAK
+    out["b_visit_note"] = ("8 B x 500 trees x 8 levels + X + out per row: the node bytes are "
+                           "read from LDS (the stage), not HBM, so this 'HBM' fraction exceeds 1 "
+                           "and bounds nothing; the binding resource is `bound` (LDS array)")
+    if n_str > 1:
+        pmc = load_pmc(pmc_path)
+        ts = {"streams": n_str, "ms_per_step": step_s * 1e3,
+              "batch_ms_one_stream": kernel_ms}
+        if pmc and pmc.get("lds_idx_active_per_launch") and not out.get("error"):
+            lds = pmc["lds_idx_active_per_launch"] * rows / pmc["rows"]
+            ts["lds_array_frac"] = lds / (CUS * CLOCK_HZ * step_s)
+            ts["lds_array_frac_one_stream"] = lds / (CUS * CLOCK_HZ * kernel_ms * 1e-3)
+            ts["basis"] = ("PMC pass LDS-array cycles per batch / (256 CUs x 2.4 GHz x the "
+                           "step time of each mode)")
+        if two_stream:
+            ts["batch_ms_two_streams"] = two_stream["batch_ms_mean"]
+            ts["batch_ms_two_streams_max"] = two_stream["batch_ms_max"]
+            ts["batch_latency_basis"] = two_stream["basis"]
+        out["two_stream"] = ts
+    return out
 
 
 def config_roofline(kernel_ms: float, rows: int, info: dict, workload: str, pmc_path: str):
@@ -497,7 +580,37 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
             "predict_ms_p50": float(np.percentile(batch_ms, 50)),
             "predict_ms_p99": float(np.percentile(batch_ms, 99)), "gc_frozen": freeze_gc,
             "p999_ms": float(np.percentile(lat_ms, 99.9)), "worst": worst,
-            "path": "in-process batcher -> ti_predict (host buffers), 1 GPU, no HTTP/JSON"}
+            "path": "in-process batcher -> ti_predict (host buffers), 1 GPU, no HTTP/JSON",
+            "_lat_ms": lat_ms}
+
+
+def pool_latency(mine: dict, world: int, rank: int, device):
+    """The C5 leg over all ranks: every rank's request latencies gathered to
+    rank 0 (all_gather_object, outside any timed region) and the percentiles
+    taken over the pooled requests; rows/s is the sum over ranks, the offered
+    rate the sum of the ranks' rates."""
+    import torch.distributed as dist
+    lat = mine.pop("_lat_ms")
+    if world == 1 or not dist.is_initialized():
+        mine.update(devices=1, qps_offered_per_gpu=mine["qps_offered"])
+        return mine
+    got = [None] * world
+    dist.all_gather_object(got, (lat, mine["rows_per_s"], mine["p99_ms"], mine["batches"]))
+    if rank != 0:
+        return None
+    allm = np.concatenate([g[0] for g in got])
+    out = dict(mine)
+    out.update(devices=world, qps_offered_per_gpu=mine["qps_offered"],
+               qps_offered=mine["qps_offered"] * world, requests=int(allm.size),
+               p50_ms=float(np.percentile(allm, 50)), p90_ms=float(np.percentile(allm, 90)),
+               p99_ms=float(np.percentile(allm, 99)), p999_ms=float(np.percentile(allm, 99.9)),
+               max_ms=float(allm.max()), rows_per_s=float(sum(g[1] for g in got)),
+               p99_ms_per_rank=[float(g[2]) for g in got],
+               batches=int(sum(g[3] for g in got)),
+               path=f"{world} ranks, each an in-process batcher -> ti_predict (host buffers) "
+                    "on its own GPU, no HTTP/JSON; percentiles over all ranks' requests "
+                    "(rank 0's batch statistics and worst request)")
+    return out
 
 
 def host_to_host(dev, X_host, rows, reps=3):
@@ -600,8 +713,11 @@ def c4_forest():
 
 
 def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_sync,
-               make_engine, cpu_fn=None, pmc_workload=None, pmc_path=None, dtype="float32"):
-    """Strong scaling: this rank's block of the batch, K steps, max-over-ranks wall."""
+               make_engine, cpu_fn=None, pmc_workload=None, pmc_path=None, dtype="float32",
+               cpu_cap=2_000_000):
+    """Strong scaling: this rank's block of the batch, K steps, max-over-ranks wall.
+    The CPU baseline is not timed here: rank 0 keeps a host sample of its
+    block (at most cpu_cap rows) and run() times it at the end."""
     import torch
     from kfserving_amd.forest import OUT_PREDICT, TI_F32, TI_F64
     lo, hi = strong_shard(total_rows, rank, world)
@@ -633,13 +749,39 @@ def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_
                                    / (kms * 1e-3) / 1e9 if kms else None)}
         if pmc_path and kms:
             res["roofline"] = config_roofline(kms, rows, eng.info(), pmc_workload, pmc_path)
-        if cpu_fn is not None and world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_fn(lambda n: X[:min(rows, n)].cpu().numpy())
+        if cpu_fn is not None and not args.no_cpu_baseline:
+            # timed later (run: after every rank's GPU legs, on the full host):
+            # keep a host copy of this rank's block, up to the sample cap
+            res["_cpu"] = (cpu_fn, X[:min(rows, cpu_cap)].cpu().numpy())
     del X, out
     eng.close()
     if device != "cpu":
         torch.cuda.empty_cache()
     return res
+
+
+def sample_taker(Xh: np.ndarray):
+    """take(n): the first n rows of a host sample, tiled when the sample (a
+    rank's block at large N) is shorter than n."""
+    def take(n):
+        n = int(n)
+        if n <= Xh.shape[0]:
+            return Xh[:n]
+        reps = -(-n // Xh.shape[0])
+        return np.concatenate([Xh] * reps)[:n]
+    return take
+
+
+def baseline_threads() -> int:
+    """Host threads for the CPU baselines: the whole host share of the job.
+    launch_ranks records it in BENCH_HOST_THREADS before it splits
+    OMP_NUM_THREADS over the ranks; under an outside launcher it is
+    OMP_NUM_THREADS (the box's share, which torchrun leaves alone when set)
+    or the affinity mask."""
+    env = os.environ.get("BENCH_HOST_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return host_threads()
 
 
 def _scaled_sample(fn, take, target_s, probe=20_000, cap=10_000_000):
@@ -665,12 +807,14 @@ def _scaled_sample(fn, take, target_s, probe=20_000, cap=10_000_000):
 def c3_cpu(trees, target_s, dtype="float32"):
     def fn(take):
         from oracle import port
-        n, dt = _scaled_sample(lambda Xs: port.lgb_predict_raw(trees, 1, 100, Xs.astype(np.float64)),
-                               take, target_s)
-        return {"value": n / dt, "unit": "rows/s", "cores": port.num_threads(),
+        thr = baseline_threads()
+        n, dt = _scaled_sample(
+            lambda Xs: port.lgb_predict_raw(trees, 1, 100, Xs.astype(np.float64), nthread=thr),
+            take, target_s)
+        return {"value": n / dt, "unit": "rows/s", "cores": thr,
                 "kind": "port", "sample": f"{n} rows of the same {dtype} batch, "
                                           "oracle/c/tree_port.c (lightgbm predict loop restated, "
-                                          f"OpenMP), {dt:.1f} s"}
+                                          f"OpenMP {thr} threads), {dt:.1f} s"}
     return fn
 
 
@@ -696,7 +840,7 @@ def c4_cpu(raw_trees, target_s):
         if os.path.exists(mk.MODEL) and os.path.exists(mk.CHECK):
             est = mk.sklearn_estimator()
             same = mk.check(est)
-            thr = host_threads()
+            thr = baseline_threads()
             est.set_params(n_jobs=thr)
             n, dt = _scaled_sample(est.predict, take, target_s, probe=4096)
             import sklearn
@@ -707,10 +851,11 @@ def c4_cpu(raw_trees, target_s):
                           f"(rebuilt from its arrays; equal to the fitted estimator on the "
                           f"check rows: {same}), {dt:.1f} s"}
         from oracle import port
-        n, dt = _scaled_sample(lambda Xs: port.sk_predict(raw_trees, 1, 64, Xs), take,
-                               min(target_s, 5.0), probe=4096)
+        pthr = baseline_threads()
+        n, dt = _scaled_sample(lambda Xs: port.sk_predict(raw_trees, 1, 64, Xs, nthread=pthr),
+                               take, min(target_s, 5.0), probe=4096)
         res["cpu_baseline_port"] = {
-            "value": n / dt, "unit": "rows/s", "cores": port.num_threads(), "kind": "port",
+            "value": n / dt, "unit": "rows/s", "cores": pthr, "kind": "port",
             "sample": f"{n} rows, oracle/c/tree_port.c (sklearn forest predict restated), "
                       f"{dt:.1f} s"}
         return res
@@ -749,10 +894,12 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
     rows, seed = shard_rows(args.rows, rank, world)
     X_host = np.random.default_rng(seed).standard_normal((rows, N_FEAT), dtype=np.float32)
     X = torch.from_numpy(X_host).to(device)
-    # consecutive steps read different copies of the batch: 3 x 112 MB is more
-    # than the 256 MB Infinity Cache, so a step's X comes from HBM, not from
-    # the previous step's cache lines
-    Xs = [X] + [X.clone() for _ in range(max(0, args.x_buffers - 1))]
+    # consecutive steps read different batches: 3 x 112 MB is more than the
+    # 256 MB Infinity Cache, so a step's X comes from HBM, not from the
+    # previous step's cache lines.  Each buffer is its own batch (seeded), so
+    # the check after the timed region can tell the batches in flight apart
+    Xs = [X] + [device_normal(rows, N_FEAT, seed * 7919 + i, device)
+                for i in range(1, max(1, args.x_buffers))]
     out = torch.empty(rows, dtype=torch.float32, device=device)
     sh = torch.cuda.current_stream().cuda_stream if device != "cpu" else 0
     it = [0]
@@ -762,8 +909,11 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
     strs = [None] + [torch.cuda.Stream(device=device) for _ in range(n_str - 1)]
     outs = [out] + [torch.empty_like(out) for _ in range(n_str - 1)]
 
+    last_x = [None] * n_str     # the X buffer each stream's last launch read
+
     def launch(k):
-        Xi = Xs[it[0] % len(Xs)]
+        last_x[k] = it[0] % len(Xs)
+        Xi = Xs[last_x[k]]
         it[0] += 1
         dev.predict_device(Xi.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
                            outs[k].data_ptr(), rows, slot=0,
@@ -803,18 +953,29 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             step()
         wall, _ = timed_steps(step, args.steps, dev_sync, events(), fork, join)
         wall = max_over_ranks(wall, device)
-    # every X buffer is a copy of one batch: each stream's last output must be
-    # the same rows, bit for bit (no batch in flight was skipped or cut short)
-    outputs_identical = all(bool(torch.equal(outs[0], o)) for o in outs[1:])
+    # each stream's last output against a one-stream predict of the batch it
+    # read (every X buffer is a distinct batch): no batch in flight was
+    # skipped, cut short or written by the other stream
+    outputs_identical = streams_match(dev, Xs, outs, last_x, rows, sh, dev_sync, device != "cpu")
     value = rows * world * args.steps / wall
+    two_stream = None
+    if n_str > 1:
+        two_stream = batch_latency_events(launch, n_str, strs, args.steps, dev_sync)
 
     # the serving-latency leg runs right after the headline, before the legs
     # that load the host (CPU baselines' thread pools, the 8M-row host
     # pipeline) or hold tens of GB on the device (C3 / C4): its p99 then
     # measures the batcher and the engine, not what ran before it
     latency = None
-    if rank == 0 and args.latency_qps > 0 and device != "cpu":
-        latency = batched_latency(dev, N_FEAT, args.latency_qps, args.latency_seconds)
+    if args.latency_qps > 0:
+        # C5 on every GPU at once: each rank is one serving worker with its own
+        # batcher in front of its own GPU (KFServer's pre-forked workers, one
+        # GPU each), offered latency_qps; the latencies of all ranks are
+        # pooled on rank 0
+        barrier_sync(dev_sync)
+        mine = batched_latency(dev, N_FEAT, args.latency_qps, args.latency_seconds,
+                               seed=7 + 1000 * rank)
+        latency = pool_latency(mine, world, rank, device)
 
     nan_variant = None
     if args.nan_variant > 0 and rank == 0 and device != "cpu":
@@ -866,22 +1027,39 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             f4, raw4, src = c4_forest()
             r = run_config(f4, 64, args.rows4, 2, args, world, rank, device, dev_sync,
                            make_engine, c4_cpu(raw4, args.cpu_seconds / 2), "c4",
-                           pmc_path("c4"))
+                           pmc_path("c4"), cpu_cap=10_000_000)
             if r is not None:
-                cb = r.pop("cpu_baseline", None)
-                if cb:
-                    r.update(cb)
                 r.update(config="C4 sklearn RandomForestRegressor 200 trees max_depth 16, "
                                 "64 features, float32 input, float64 mean", model=src)
         else:
             raise ValueError(f"unknown config {name!r}")
         configs[name] = r
 
+    # the CPU baselines, at every world size: after the last rank's GPU legs,
+    # on rank 0 alone with the whole host share (the other ranks have left
+    # the process group and exit; none of them spins on a device sync)
+    barrier_sync(dev_sync)
+    dev.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank != 0:
+        return None
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline(trees, ti, X_host, args.cpu_seconds)
+        for name, r in configs.items():
+            if r is not None and "_cpu" in r:
+                fn, Xh = r.pop("_cpu")
+                got = fn(sample_taker(Xh))
+                if "cpu_baseline" in got or "cpu_baseline_port" in got:
+                    r.update(got)               # C4: the library and the port
+                else:
+                    r["cpu_baseline"] = got
+    for r in configs.values():
+        if r is not None:
+            r.pop("_cpu", None)
     line = None
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(trees, ti, X_host, args.cpu_seconds)
         line = {
             "metric": "predicted rows/sec (500-tree XGB, 28 feat)",
             "value": value,
@@ -906,16 +1084,14 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
                               "value": rows * world * args.steps / wall1,
                               "kernel_ms": kernel_ms},
             "streams_outputs_identical": outputs_identical,
-            "roofline": roofline(kernel_ms, rows, info, args.pmc_json),
+            "roofline": headline_roofline(kernel_ms, rows, info, args.pmc_json, wall / args.steps,
+                                          two_stream, n_str),
             "cpu_baseline": cpu,
             "batched_latency": latency,
             "nan_variant": nan_variant,
             "host_pipeline": host_pipeline,
         }
         line.update(configs)
-    dev.close()
-    if world > 1:
-        dist.destroy_process_group()
     return line
 
 
@@ -937,7 +1113,10 @@ def launch_ranks(n: int, argv) -> int:
            os.path.abspath(__file__)] + list(argv)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    env.setdefault("OMP_NUM_THREADS", str(max(1, host_threads() // n)))
+    # the CPU baselines run on rank 0 after the GPU legs with the whole host
+    # share; the ranks' own host work gets an equal part of it
+    env.setdefault("BENCH_HOST_THREADS", str(host_threads()))
+    env["OMP_NUM_THREADS"] = str(max(1, host_threads() // n))
     return subprocess.run(cmd, env=env).returncode
 
 

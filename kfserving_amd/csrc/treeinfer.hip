@@ -1975,9 +1975,10 @@ int upload_device(ti_forest* f, DeviceForest& d, int device) {
   } else if (f->layout == 3) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = upload(&d.bh_img[i], f->bh[i].img, &d.bytes))) return rc;
-    if ((rc = upload(&d.bh_fix_img, f->bh[0].fix_img, &d.bytes))) return rc;
       if ((rc = upload(&d.bh_tbl[i], f->bh[i].tbl, &d.bytes))) return rc;
     }
+    // the permuted image of the fixed walk (float32 view only): once per replica
+    if ((rc = upload(&d.bh_fix_img, f->bh[0].fix_img, &d.bytes))) return rc;
     if ((rc = upload(&d.heap_leaf_ids, f->h_heap_leaf_ids, &d.bytes))) return rc;
   } else {
     if ((rc = upload(&d.nodes, f->h_nodes, &d.bytes))) return rc;
@@ -2729,6 +2730,10 @@ int ensure_shap(ti_forest* f) {
   int dev0 = 0;
   TI_HIP(hipGetDevice(&dev0));
   int rc = TI_OK;
+  // each replica's byte count before the uploads: a failure restores it, so
+  // ti_forest_info's device_bytes does not keep the freed tables
+  std::vector<int64_t> bytes0;
+  for (auto& dp : f->devs) bytes0.push_back(dp->bytes);
   for (auto& dp : f->devs) {
     DeviceForest& d = *dp;
     if ((rc = fail_hip(hipSetDevice(d.device), "hipSetDevice"))) break;
@@ -2742,9 +2747,10 @@ int ensure_shap(ti_forest* f) {
     // nothing half-built survives: every replica's path tables are freed (the
     // host tables stay, so the next call retries from them)
     const std::string err = g_last_error;
-    for (auto& dp : f->devs) {
-      (void)hipSetDevice(dp->device);
-      free_shap(*dp);
+    for (size_t i = 0; i < f->devs.size(); ++i) {
+      (void)hipSetDevice(f->devs[i]->device);
+      free_shap(*f->devs[i]);
+      f->devs[i]->bytes = bytes0[i];
     }
     (void)hipGetLastError();
     (void)hipSetDevice(dev0);

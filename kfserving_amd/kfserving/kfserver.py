@@ -283,12 +283,13 @@ class Application:
             return bad(str(e))
         forest = getattr(model, "_forest", None)
         width = getattr(forest, "n_features", None)
-        if self._batcher_factory is not None and (width is None or X.shape[1] == width):
+        if self._batcher_factory is not None and width is not None and X.shape[1] == width:
             # one tensor batcher per model, for requests of the model's own
             # width; a request of another width (fewer columns read as missing,
             # as the libraries read them) is predicted alone, so a client's
             # widths can neither fail a batch of well-formed requests nor grow
-            # the batcher table
+            # the batcher table.  A model that does not state its width is not
+            # batched: requests of different widths could share a batch
             key = (name, "tensor")
             batcher = self._batchers.get(key)
             if batcher is None or batcher.model is not model:

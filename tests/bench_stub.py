@@ -4,6 +4,8 @@ nothing on a device, sleeps per call so the slower rank's wall time is known
 (local rank 1: 20 ms a predict, others 1 ms)."""
 import time
 
+import numpy as np
+
 
 class StubEngine:
     def __init__(self, forest, rank):
@@ -15,6 +17,11 @@ class StubEngine:
                        out_len, slot=0, stream=0):
         self.calls.append((n_rows, n_cols))
         time.sleep(0.02 if self.rank == 1 else 0.001)
+
+    def predict(self, X, kind=0):
+        """Host-buffer predict (bench.py's C5 leg): 1 ms a batch, zeros."""
+        time.sleep(0.001)
+        return np.zeros(np.asarray(X).shape[0], dtype=np.float32)
 
     def info(self):
         return {"layout": 3}

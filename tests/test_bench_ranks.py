@@ -79,8 +79,9 @@ def test_bench_rank_path_two_ranks():
     # the max over ranks: rank 1's 5 x 20 ms dominates
     assert line["ms_per_step"] >= 20.0
     assert abs(line["value"] - 4096 * 2 * 5 / (line["ms_per_step"] * 5e-3)) < 1e-6 * line["value"]
-    # no GPU: one stream, and the one-stream region is the headline's
-    assert line["config"]["streams"] == 1 and line["streams_outputs_identical"] is True
+    # no GPU: one stream, and the one-stream region is the headline's; the
+    # stand-in engine writes no outputs, so there is nothing to compare
+    assert line["config"]["streams"] == 1 and line["streams_outputs_identical"] is None
     assert line["single_stream"]["value"] == line["value"]
     # C3: strong scaling, 500 rows per rank, 1 untimed + 2 timed steps
     assert calls0[1] == [(500, 100)] * 3 and calls1[1] == [(500, 100)] * 3
@@ -98,11 +99,14 @@ def test_bench_cli_gpus_n_starts_n_ranks():
     n_gpus is 2 and value = both ranks' rows / the slowest rank's wall."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "4"                           # the job's host share
+    env.pop("BENCH_HOST_THREADS", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
            "--engine", "tests.bench_stub:make", "--steps", "5", "--warmup", "1",
-           "--rows", "2048", "--configs", "", "--no-cpu-baseline", "--latency-qps", "0",
+           "--rows", "2048", "--configs", "c3", "--rows3", "2000", "--config-steps", "1",
+           "--cpu-seconds", "0.2", "--latency-qps", "200", "--latency-seconds", "0.5",
            "--nan-variant", "0", "--host-rows", "0"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout                      # rank 0 alone prints
@@ -112,6 +116,20 @@ def test_bench_cli_gpus_n_starts_n_ranks():
     assert line["ms_per_step"] >= 20.0                    # rank 1's 20 ms steps dominate
     want = 2048 * 2 * 5 / (line["ms_per_step"] * 5e-3)
     assert abs(line["value"] - want) < 1e-6 * want
+    # the CPU baselines at N > 1, timed on rank 0 with the
+    # whole host share (not OMP_NUM_THREADS / N), the thread count stated
+    cb = line["cpu_baseline"]
+    assert cb is not None and cb["value"] > 0 and cb["cores"] == 4 and cb["kind"] == "port"
+    c3 = line["c3"]
+    assert c3["rows"] == 2000 and c3["rows_per_gpu"] == 1000
+    assert c3["cpu_baseline"]["value"] > 0 and c3["cpu_baseline"]["cores"] == 4
+    assert "_cpu" not in c3
+    # the C5 leg drives every rank's device, pooled on rank 0
+    bl = line["batched_latency"]
+    assert bl["devices"] == 2 and len(bl["p99_ms_per_rank"]) == 2
+    assert bl["qps_offered"] == 2 * bl["qps_offered_per_gpu"] == 400
+    assert bl["p50_ms"] <= bl["p99_ms"] <= bl["max_ms"] and bl["requests"] > 0
+    assert "_lat_ms" not in bl
 
 
 def test_headline_defaults_two_streams():

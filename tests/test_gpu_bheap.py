@@ -213,3 +213,32 @@ def test_bheap_fixed_walk(quantize, ng):
                                xgb_ref.predict(r3, X), rtol=1e-5, atol=0)
     # leaf ids keep the indexed walk
     assert np.array_equal(dev.predict(X[:, :28], OUT_LEAF), xgb_ref.leaf_index(ref, X[:, :28]))
+
+
+def test_fix_image_uploaded_once_and_freed():
+    # the fixed walk's permuted image was uploaded inside the
+    # per-view loop, so each replica held (and leaked) a second copy.  With
+    # the permutation on, a replica holds exactly one more tree image than
+    # without it, and create/predict/destroy cycles give the memory back.
+    import torch
+    trees, ti, forest, ref = _xgb(500, 8, 28, seed=5)
+    X = _edge_rows(trees, 8, 28, 1024, seed=2)
+
+    def make(perm):
+        d = _with_env({"TI_FIX_PERM": perm}, lambda: DeviceForest(forest, [0]))
+        d.predict(X, OUT_MARGIN)              # the replica is created on first use
+        return d
+
+    on, off = make("1"), make("0")
+    ion, ioff = on.info(), off.info()
+    assert ion["walk"] == 2 and ion["tree_stride_bytes"] > 0
+    assert ion["device_bytes"] - ioff["device_bytes"] == 500 * ion["tree_stride_bytes"]
+    on.close()
+    off.close()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    for _ in range(8):
+        make("1").close()
+    torch.cuda.synchronize()
+    # 8 leaked 1 MB images would show; allow the allocator's own slack
+    assert free0 - torch.cuda.mem_get_info(0)[0] < 4 * 500 * ion["tree_stride_bytes"]

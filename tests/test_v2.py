@@ -155,6 +155,7 @@ def test_v2_requests_share_batches(serve):
     server = KFServer(registered_models=KFModelRepository(), max_batchsize=64,
                       max_latency_ms=50)
     model = RowSum()
+    model._forest = _Width(5)            # the tensor batcher takes the model's own width
     server.register_model(model)
     s = serve(server)
     rng = np.random.default_rng(3)
@@ -175,6 +176,38 @@ def test_v2_requests_share_batches(serve):
         assert np.array_equal(np.frombuffer(raw, "<f8"), X.sum(axis=1) * 2)
     assert len(model.batches) < len(Xs)                 # coalesced
     assert sum(model.batches) == sum(X.shape[0] for X in Xs)
+
+
+class _Width:
+    def __init__(self, n):
+        self.n_features = n
+
+
+def test_v2_model_without_width_is_not_batched(serve):
+    """a model that states no width gets no tensor batcher, so
+    requests of different widths never share (and fail) one batch."""
+    server = KFServer(registered_models=KFModelRepository(), max_batchsize=64,
+                      max_latency_ms=50)
+    model = RowSum()
+    server.register_model(model)
+    s = serve(server)
+    rng = np.random.default_rng(4)
+    Xs = [rng.standard_normal((2, w)) for w in (3, 4, 3, 6, 5, 3)]
+    res = [None] * len(Xs)
+
+    def one(i):
+        body, hdrs = _binary_request(Xs[i])
+        res[i] = s.fetch("/v2/models/m/infer", "POST", body, hdrs)
+    th = [threading.Thread(target=one, args=(i,)) for i in range(len(Xs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for X, (code, rh, out) in zip(Xs, res):
+        assert code == 200, out
+        _, raw = _split_response(rh, out)
+        assert np.array_equal(np.frombuffer(raw, "<f8"), X.sum(axis=1) * 2)
+    assert model.batches == [2] * len(Xs)               # each request alone
 
 
 def test_v2_decode_units():
