@@ -88,7 +88,8 @@ def launched_kernel(info: dict) -> str:
     if layout == 3:
         return WALK_KERNELS.get(info.get("walk"), "bheap_predict_kernel")
     if layout == 9:
-        return "t8explicit_predict_kernel" if info.get("bottom") == 1 else "texplicit_predict_kernel"
+        return {1: "t8explicit_predict_kernel", 2: "t16explicit_predict_kernel"}.get(
+            info.get("bottom"), "texplicit_predict_kernel")
     return LAYOUT_KERNELS.get(layout, f"layout{layout}")
 
 

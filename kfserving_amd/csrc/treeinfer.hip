@@ -631,7 +631,8 @@ struct ti_forest {
   std::vector<uint32_t> h_tx_off, h_tx_nint;
   // layout 9's compact u8 bottom (plan_tx8): per tree the first bottom
   // position [T+1], and per bottom position the leaf value (ACC) / ordinal
-  int32_t tx8 = 0;
+  int32_t tx8 = 0;                 // 1: compact u8 bottom, 2: compact u16 bottom
+  uint32_t tx16_mask = 0;          //   u16: the bottom word's bin-offset bits (KArgs bin_mask)
   std::vector<uint32_t> h_tx8_pos;
   std::vector<unsigned char> h_tx8_val;
   std::vector<int32_t> h_tx8_ord;
@@ -1609,10 +1610,32 @@ bool plan_tx(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>&
 // 0, k' = p / 2; its value and ordinal are read by position from global
 // tables when the group is walked.  Returns false (u8 layout 9 keeps its
 // records) when a tree has more than 255 leaves or the images do not fit.
-bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>& slot_of, int D) {
-  if (env_int("TI_TX8", 1) == 0 || !f->rx[0].b8 || !f->rx[1].b8) return false;
+//
+// The u16 form (b16, plan_tx16; t16explicit_predict_kernel) keeps the u16
+// record x word's rank (high half), word index, half-word bit and NaN-left
+// (low half, lane part cleared) and puts k' into bits 2-9 of the lane part;
+// a leaf is rank 0xFFFF (even) / 0 (odd) with bin offset 0, and no internal
+// node may have either rank (the leaf test).  It needs tiles of >= 256 rows
+// (bits 2-9 inside the lane part).  Zero-missing forests lose the word's zero-flip
+// bit: a 64-byte table of one bit per position sits between the top and the
+// bottom (kT16ZfBytes), read only by the slow step.
+bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>& slot_of, int D,
+              bool b16 = false) {
+  if (!b16 && (env_int("TI_TX8", 1) == 0 || !f->rx[0].b8 || !f->rx[1].b8)) return false;
+  uint32_t bmask16 = 0, wmask16 = 0;
+  if (b16) {
+    if (env_int("TI_TX16", 1) == 0 || f->rx[0].b8 || f->rx[1].b8) return false;
+    const int R = f->rx[0].rows;
+    if (f->rx[1].rows != R || R < 256 || (R & (R - 1))) return false;
+    int lg = 0;
+    while ((1 << lg) < R) ++lg;
+    wmask16 = (0xFFFFu << (2 + lg)) & 0xFFFFu;   // the word index bits
+    bmask16 = wmask16 | 2u;
+  }
+  const uint32_t zfb = (b16 && f->zero_rule) ? ti::kT16ZfBytes : 0u;
   int D0 = env_int("TI_TX_TOP", 6);
-  D0 = std::max(1, std::min(D0, std::min(D, 10)));
+  // (the u16 bottom also runs without a top: D0 = 0, the root the only entry)
+  D0 = std::max(b16 ? 0 : 1, std::min(D0, std::min(D, 10)));
   const int T = d->n_trees;
   const size_t NE = size_t(1) << D0;
   const uint32_t topb = static_cast<uint32_t>(8 * NE);
@@ -1668,7 +1691,7 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
       lvl.swap(nxt);
     }
     pos[t + 1] = pos[t] + static_cast<uint32_t>(ord.size());
-    const uint64_t bytes = topb + ((static_cast<uint64_t>(ord.size()) * 4 + 15) & ~uint64_t(15));
+    const uint64_t bytes = topb + zfb + ((static_cast<uint64_t>(ord.size()) * 4 + 15) & ~uint64_t(15));
     if (bytes > 65520 || off[t] + bytes > 0xFFFFFFF0ull) return false;
     off[t + 1] = off[t] + static_cast<uint32_t>(bytes);
   }
@@ -1688,7 +1711,11 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
   // its stage walks duplicate trees): on c3_maxbin at 12 trees a stage, ILP 4
   // 4.70 ms, 7 5.29, 8 5.72 (profiles/r3_tx8_sweep.jsonl)
   const int force_ilp = env_int("TI_LX_ILP", 0);
-  const int ilp = force_ilp > 0 ? (force_ilp >= 8 ? 8 : force_ilp == 7 ? 7 : 4) : 4;
+  int ilp = force_ilp > 0 ? (force_ilp >= 8 ? 8 : force_ilp == 7 ? 7 : 4) : 4;
+  if (b16) {   // the u16 kernel is instantiated at 4, 8, 12 and 16 trees a lane
+    const int i16 = env_int("TI_TX16_ILP", 8);
+    ilp = i16 >= 16 ? 16 : i16 >= 12 ? 12 : i16 >= 8 ? 8 : 4;
+  }
   std::vector<int32_t> stages(1, 0);
   int t0 = 0;
   while (t0 < T) {
@@ -1726,21 +1753,35 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
       const int64_t b = d->tree_offset[t];
       const int32_t n = static_cast<int32_t>(d->tree_offset[t + 1] - b);
       uint32_t* top = &rx.top[off[t] / 4];
-      uint32_t* bot = top + 2 * NE;
+      unsigned char* zf = reinterpret_cast<unsigned char*>(top + 2 * NE);
+      uint32_t* bot = top + 2 * NE + zfb / 4;
       const std::vector<int32_t>& ord = order[t];
       entry_of.assign(n, -1);
+      // a leaf word at position p: self-looping (even: rank 0xFF / 0xFFFF,
+      // NaN-left; odd: rank 0), its own pair index
+      auto leaf_word = [&](uint32_t p) {
+        if (b16) return (p & 1 ? 0u : (0xFFFF0000u | 1u)) | ((p >> 1) << 2);
+        return kLeaf | (p & 1 ? 0u : (0xFF0000u | kNanLeft)) | ((p >> 1) << 24);
+      };
       for (uint32_t p = 0; p < ord.size(); ++p) {
         const int32_t v = ord[p];
         if (v < 0) {
-          bot[p] = kLeaf | (p & 1 ? 0u : (0xFF0000u | kNanLeft)) | ((p >> 1) << 24);
+          bot[p] = leaf_word(p);
           continue;
         }
         if (entry_of[v] < 0) entry_of[v] = static_cast<int32_t>(p);
         const int64_t g = b + v;
-        if (d->feature[g] < 0)
-          bot[p] = kLeaf | (p & 1 ? 0u : (0xFF0000u | kNanLeft)) | ((p >> 1) << 24);
-        else
+        if (d->feature[g] < 0) {
+          bot[p] = leaf_word(p);
+        } else if (b16) {
+          const uint32_t xw = rx.recs[b + slot_of[g]].x;
+          const uint32_t rk = xw >> 16;
+          if (rk == 0u || rk == 0xFFFFu) return false;   // the ranks that mark a leaf
+          bot[p] = (xw & (0xFFFF0000u | wmask16 | 3u)) | (kpair[t][v] << 2);
+          if (zfb && (xw & ti::kRxZeroFlip)) zf[p >> 3] |= static_cast<unsigned char>(1u << (p & 7));
+        } else {
           bot[p] = rx.recs[b + slot_of[g]].x | (kpair[t][v] << 24);
+        }
       }
       // the top: x words, and at depth D0 the entry position
       struct TItem { int32_t v; uint32_t hp; int l; };
@@ -1754,7 +1795,7 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
           continue;
         }
         const bool leaf = d->feature[g] < 0;
-        top[it.hp] = leaf ? kHxPad8 : rx.recs[b + slot_of[g]].x;
+        top[it.hp] = leaf ? (b16 ? kHxPad : kHxPad8) : rx.recs[b + slot_of[g]].x;
         ts.push_back(TItem{leaf ? it.v : d->left[g], 2 * it.hp, it.l + 1});
         ts.push_back(TItem{leaf ? it.v : d->right[g], 2 * it.hp + 1, it.l + 1});
       }
@@ -1767,7 +1808,8 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
   f->lx_stage_cap = static_cast<int64_t>(cap);
   f->lx_ilp = ilp;
   f->hx_top = D0;
-  f->tx8 = 1;
+  f->tx8 = b16 ? 2 : 1;
+  f->tx16_mask = bmask16;
   f->layout = 9;
   return true;
 }
@@ -2053,6 +2095,13 @@ KernelFn select_t8explicit(int xdt, int accum, int K, bool z, int ilp) {   // la
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(11, K, true, z, false, ilp);
   if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(11, K, true, z, false, ilp);
   return ti::kernels_df(11, K, true, z, false, ilp);
+}
+
+KernelFn select_t16explicit(int xdt, int accum, int K, bool z, int ilp) {   // layout 9, compact u16 bottom
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(12, K, true, z, true, ilp);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(12, K, true, z, true, ilp);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(12, K, true, z, true, ilp);
+  return ti::kernels_df(12, K, true, z, true, ilp);
 }
 
 KernelFn select_hexplicit(int xdt, int accum, int K, bool z, int ilp) {
@@ -2346,7 +2395,9 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.tx_pos = d.tx8_pos;
     a.tx_vals = d.tx8_val;
     a.tx_ord = d.tx8_ord;
-    KernelFn fn = f->tx8 ? select_t8explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
+    a.bin_mask = f->tx16_mask;
+    KernelFn fn = f->tx8 == 2 ? select_t16explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
+                : f->tx8 ? select_t8explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
                          : select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp, rx.b8 != 0);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
@@ -2538,13 +2589,101 @@ int predict_pipelined(ti_forest* f, int slot, DeviceForest& d, const unsigned ch
   return rc ? rc : (r1 ? r1 : r2);
 }
 
+// The caller's own buffers page-locked for the call (hipHostRegister), so
+// chunks go H2D straight from X and D2H straight into out, alternating two
+// lanes with no host copy and no host wait until the end (TI_HOST_REGISTER=1;
+// A/B against the pinned-chunk pipeline, which copies every byte once on the
+// host).  Returns TI_ERR_UNSUPPORTED, having done nothing, when a buffer
+// cannot be registered; the caller then takes the pinned-chunk pipeline.
+int predict_registered(ti_forest* f, int slot, DeviceForest& d, const unsigned char* X, int xdt,
+                       int64_t rows, int32_t cols, int64_t stride, int kind, unsigned char* out,
+                       int64_t ch) {
+  const size_t xs = dtype_size(xdt);
+  const size_t os = dtype_size(output_dtype(f, kind)) * output_width(f, kind);
+  const size_t x_row = static_cast<size_t>(stride) * xs;
+  const size_t x_bytes = static_cast<size_t>((rows - 1) * stride + cols) * xs;
+  const size_t o_bytes = static_cast<size_t>(rows) * os;
+  const uintptr_t pg = 4096;
+  struct Reg {
+    void* p = nullptr;
+    bool mine = false;
+    ~Reg() {
+      if (mine) (void)hipHostUnregister(p);
+    }
+  } rx, ro;
+  auto reg = [&](Reg& r, const void* base, size_t n) -> bool {
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(base) & ~(pg - 1);
+    const uintptr_t hi = (reinterpret_cast<uintptr_t>(base) + n + pg - 1) & ~(pg - 1);
+    r.p = reinterpret_cast<void*>(lo);
+    const hipError_t e = hipHostRegister(r.p, hi - lo, hipHostRegisterDefault);
+    if (e == hipSuccess) {
+      r.mine = true;
+      return true;
+    }
+    (void)hipGetLastError();
+    return e == hipErrorHostMemoryAlreadyRegistered;
+  };
+  if (!reg(rx, X, x_bytes) || !reg(ro, out, o_bytes)) return TI_ERR_UNSUPPORTED;
+  struct LaneSync {
+    DeviceForest& d;
+    ~LaneSync() {
+      for (int l = 0; l < 2; ++l)
+        if (d.lane_stream[l]) (void)hipStreamSynchronize(d.lane_stream[l]);
+    }
+  } lane_sync{d};
+  const size_t x_cap = static_cast<size_t>(ch) * x_row;
+  const size_t o_cap = static_cast<size_t>(ch) * os;
+  if (d.lane_x_cap < x_cap || d.lane_o_cap < o_cap) {
+    for (int l = 0; l < 2; ++l) {
+      if (d.lane_hx[l]) (void)hipHostFree(d.lane_hx[l]);
+      if (d.lane_ho[l]) (void)hipHostFree(d.lane_ho[l]);
+      if (d.lane_dx[l]) (void)hipFree(d.lane_dx[l]);
+      if (d.lane_do[l]) (void)hipFree(d.lane_do[l]);
+      d.lane_hx[l] = d.lane_ho[l] = d.lane_dx[l] = d.lane_do[l] = nullptr;
+    }
+    d.lane_x_cap = d.lane_o_cap = 0;
+    for (int l = 0; l < 2; ++l) {
+      TI_HIP(hipHostMalloc(&d.lane_hx[l], x_cap, hipHostMallocDefault));
+      TI_HIP(hipHostMalloc(&d.lane_ho[l], o_cap, hipHostMallocDefault));
+      TI_HIP(hipMalloc(&d.lane_dx[l], x_cap));
+      TI_HIP(hipMalloc(&d.lane_do[l], o_cap));
+    }
+    d.lane_x_cap = x_cap;
+    d.lane_o_cap = o_cap;
+  }
+  for (int l = 0; l < 2; ++l)
+    if (!d.lane_stream[l]) TI_HIP(hipStreamCreateWithFlags(&d.lane_stream[l], hipStreamNonBlocking));
+  const int64_t n_chunks = (rows + ch - 1) / ch;
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    const int l = static_cast<int>(c & 1);
+    const int64_t r0 = c * ch;
+    const int64_t n = std::min(ch, rows - r0);
+    const size_t xb = static_cast<size_t>((n - 1) * stride + cols) * xs;
+    hipStream_t st = d.lane_stream[l];
+    TI_HIP(hipMemcpyAsync(d.lane_dx[l], X + static_cast<size_t>(r0) * x_row, xb,
+                          hipMemcpyHostToDevice, st));
+    int rc = launch_any(f, slot, d.lane_dx[l], xdt, n, cols, stride, kind, d.lane_do[l], st);
+    if (rc) return rc;
+    TI_HIP(hipMemcpyAsync(out + static_cast<size_t>(r0) * os, d.lane_do[l], static_cast<size_t>(n) * os,
+                          hipMemcpyDeviceToHost, st));
+  }
+  for (int l = 0; l < 2; ++l) TI_HIP(hipStreamSynchronize(d.lane_stream[l]));
+  return TI_OK;
+}
+
 int predict_shard(ti_forest* f, int slot, DeviceForest& d, const unsigned char* X, int xdt,
                   int64_t rows, int32_t cols, int64_t stride, int kind, unsigned char* out) {
   std::lock_guard<std::mutex> lk(d.mu);
   TI_HIP(hipSetDevice(d.device));
   {
     const int64_t ch = chunk_rows(static_cast<size_t>(stride) * dtype_size(xdt));
-    if (rows > ch) return predict_pipelined(f, slot, d, X, xdt, rows, cols, stride, kind, out, ch);
+    if (rows > ch) {
+      if (env_int("TI_HOST_REGISTER", 0)) {
+        const int rc = predict_registered(f, slot, d, X, xdt, rows, cols, stride, kind, out, ch);
+        if (rc != TI_ERR_UNSUPPORTED) return rc;
+      }
+      return predict_pipelined(f, slot, d, X, xdt, rows, cols, stride, kind, out, ch);
+    }
   }
   const size_t xs = dtype_size(xdt);
   const size_t x_elems = static_cast<size_t>((rows - 1) * stride + cols);
@@ -3208,8 +3347,8 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         if (b8) {
           f->layout = 9;   // u8 bins (planned above)
         } else if ((want == "texplicit" || (auto_ok && env_int("TI_NO_TEXPLICIT", 0) == 0)) &&
-                   plan_tx(desc, f.get(), slot_of, D)) {
-          // layout 9
+                   (plan_tx8(desc, f.get(), slot_of, D, true) || plan_tx(desc, f.get(), slot_of, D))) {
+          // layout 9 (the compact u16 bottom where it fits, else records)
         } else if ((want == "lexplicit" || auto_ok) && env_int("TI_NO_LEXPLICIT", 0) == 0 &&
                    plan_lx_stages(f.get(), f->T)) {
           f->layout = 7;

@@ -12,7 +12,8 @@ using KernelFn = void (*)(KArgs);
 // layout: 0 heap, 1 explicit, 3 binned heap, 6 record explicit, 7 staged
 // record explicit, 8 heap top + record bottom, 9 heap top + staged record
 // bottom (2, 4 and 5 were retired in round 3); 10 selects the fixed-layout
-// walk of layout 3 (bheap_fix_kernel), 11 layout 9's compact u8 bottom.
+// walk of layout 3 (bheap_fix_kernel), 11 layout 9's compact u8 bottom, 12
+// its compact u16 bottom.
 // fl: feature image in
 // LDS; z: LightGBM zero rule; b16 / pf: binned heap (and layout 9) bin width
 // and prefetch depth.
@@ -39,6 +40,18 @@ KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
     return pf >= 8 ? t8explicit_predict_kernel<XT, ACC, KMAX, false, 8>
            : pf == 7 ? t8explicit_predict_kernel<XT, ACC, KMAX, false, 7>
                      : t8explicit_predict_kernel<XT, ACC, KMAX, false, 4>;
+  }
+  if (layout == 12) {   // layout 9 with the compact u16 bottom; pf carries the tree ILP
+    if constexpr (sizeof(ACC) == 8) {
+      if (z) return pf >= 16 ? t16explicit_predict_kernel<XT, ACC, KMAX, true, 16>
+                    : pf >= 12 ? t16explicit_predict_kernel<XT, ACC, KMAX, true, 12>
+                    : pf >= 8 ? t16explicit_predict_kernel<XT, ACC, KMAX, true, 8>
+                              : t16explicit_predict_kernel<XT, ACC, KMAX, true, 4>;
+    }
+    return pf >= 16 ? t16explicit_predict_kernel<XT, ACC, KMAX, false, 16>
+           : pf >= 12 ? t16explicit_predict_kernel<XT, ACC, KMAX, false, 12>
+           : pf >= 8 ? t16explicit_predict_kernel<XT, ACC, KMAX, false, 8>
+                     : t16explicit_predict_kernel<XT, ACC, KMAX, false, 4>;
   }
   if (layout == 9) {   // pf carries the tree ILP (4, 7 or 8); b16 false: u8 bins
     if (!b16) return select_tx<XT, ACC, KMAX, true>(z, pf);

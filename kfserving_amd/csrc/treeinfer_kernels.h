@@ -1234,6 +1234,9 @@ __device__ __forceinline__ uint16_t lds_rxbin(uint32_t byte_addr) {
 #define TI_RX_POSTSTEP 1   // layout 6: the group's loop test reads the lanes after the
                            // step, so no pass runs once every lane is at its leaf
 #endif
+#ifndef TI_TC_BCAST
+#define TI_TC_BCAST 0   // compact bottoms: finished lanes read one broadcast pair (A/B)
+#endif
 #ifndef TI_RX_BINQ
 #define TI_RX_BINQ 8   // features searched at once per lane (independent load chains;
                        // 16 measured slower on C3 and C4)
@@ -2030,10 +2033,19 @@ __device__ __forceinline__ void t8_stage(const KArgs& a, ACC (&acc)[KMAX], int t
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
         b[q] = lds_u8((x[q] & W::kNodeMask) | lane_off);
+#if TI_TC_BCAST
+        // a finished lane reads the tree's first pair (one broadcast address)
+        // and keeps its leaf word: no random self-loop addresses in the banking
+        pr[q] = lx_rec(base[q] + ((x[q] & W::kLeaf) ? 0u : ((x[q] >> 24) << 3)));
+#else
         pr[q] = lx_rec(base[q] + ((x[q] >> 24) << 3));
+#endif
       }
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
+#if TI_TC_BCAST
+        const uint32_t x0 = x[q];
+#endif
         if (!SLOW) {
           asm("v_cmp_lt_u32_sdwa vcc, %0, %1 src0_sel:BYTE_2 src1_sel:DWORD\n\t"
               "v_cndmask_b32 %0, %2, %3, vcc"
@@ -2041,6 +2053,9 @@ __device__ __forceinline__ void t8_stage(const KArgs& a, ACC (&acc)[KMAX], int t
         } else {
           x[q] = t8_right_slow<ZERO>(x[q], b[q]) ? pr[q].y : pr[q].x;
         }
+#if TI_TC_BCAST
+        x[q] = (x0 & W::kLeaf) ? x0 : x[q];
+#endif
       }
     }
     uint32_t li[ILP];   // the leaf's index in the position tables
@@ -2120,6 +2135,217 @@ __global__ void __launch_bounds__(512) t8explicit_predict_kernel(const KArgs a) 
     } else {
       if (vis) t8_stage<ACC, KMAX, ZERO, false, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
       else t8_stage<ACC, KMAX, ZERO, false, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
+    }
+  }
+  if (vis) t8_flush<ACC, KMAX, ILP>(a, acc, pend, pend_t);
+  if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
+// ---- layout 9 with the compact u16 bottom (plan_tx16) -----------------------
+// The u8 compact bottom's step for u16 bins (C3: ~2,500 thresholds a feature).
+// A bottom node is one u32: rank in the high half (the compare reads WORD_1,
+// as the record walk's), the bin's byte offset in the low half with the lane
+// part cleared (bit 0 NaN-left, bit 1 the half-word, the word index above the
+// lane bits), and the children's pair index k' in bits 2-9 -- inside the lane
+// part, which the bin address masks off (a.bin_mask).  Children sit side by
+// side at positions 2k', 2k'+1, so a step is one LDS round trip (the u16 bin
+// and the 8-byte pair) and 5 VALU, against the record bottom's two round trips
+// and 7 VALU.  A leaf loops on itself (rank 0xFFFF at even positions: never
+// right, NaN-left; rank 0 at odd ones: always right, since every real bin is
+// >= 1 and a NaN takes the NaN-left bit) with bin offset 0, so a finished
+// lane reads its own column of word 0 (conflict-free, a real bin: a read of
+// anything else could return 0 and send an odd leaf to its sibling).  No
+// internal node has rank 0 or 0xFFFF (plan_tx16 checks), so the group's loop
+// ends when every tree's rank is one of those: (x + 0x10000) < 0x20000.  LightGBM's
+// zero flip has no bit left in the word: zero-missing forests keep one flag
+// bit per position in a 64-byte table between the top and the bottom, read by
+// the slow step (tiles holding an exact 0 or a NaN), which tracks the node's
+// position.  Leaf values come from the position tables as in t8_stage.
+constexpr uint32_t kT16ZfBytes = 64;   // zero-flip bits of <= 512 positions
+
+template <bool ZERO>
+__device__ __forceinline__ bool t16_right_slow(uint32_t x, uint32_t b, bool zf) {
+  constexpr uint32_t kNan = RxBins<false>::template nan_code<ZERO>();
+  bool right = (x >> 16) < b;
+  if (ZERO) right = right != (((b & 1u) != 0u) && zf);
+  if (b == kNan) right = (x & 1u) == 0u;
+  return right;
+}
+
+template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP>
+__device__ __forceinline__ void t16_stage(const KArgs& a, ACC (&acc)[KMAX], int t0, int t1,
+                                          uint32_t sbase, uint32_t lane_off, int64_t row,
+                                          bool live, ACC (&pend)[ILP], int (&pend_t)[ILP]) {
+  rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* tx_pos = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.tx_pos));
+  const int D0 = a.depth;
+  const uint32_t topb = 8u << D0;                   // 2^(D0+1) u32
+  const uint32_t zfb = ZERO ? kT16ZfBytes : 0u;     // zero-flip bits before the bottom
+  const uint32_t bmask = a.bin_mask;                // word index | half (the lane part cleared)
+  for (int j = t0; j < t1; j += ILP) {
+    uint32_t base[ILP], idx[ILP], nd[ILP];
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = (j + q) < t1 ? (j + q) : (t1 - 1);
+      base[q] = sbase + tx_off[tq];
+      idx[q] = 1u;
+      nd[q] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+          static_cast<uintptr_t>(base[q] + 4u));   // the root: one broadcast read
+    }
+    for (int l = 0; l < D0; ++l) {   // the top, as layout 9's (record x words)
+      uint32_t b[ILP];
+      rx_u2_t pr[ILP];
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        b[q] = lds_u16((nd[q] & kRxOffMask) | lane_off);
+        pr[q] = lx_rec(base[q] + 8u * idx[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        if (!SLOW) {
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %2 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+              "v_cndmask_b32 %0, %3, %4, vcc\n\t"
+              "v_addc_co_u32 %1, vcc, %1, %1, vcc"
+              : "+v"(nd[q]), "+v"(idx[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y)
+              : "vcc");
+        } else {
+          const bool right = rx_right_slow<ZERO, false>(nd[q], b[q]);
+          idx[q] = idx[q] + idx[q] + (uint32_t)right;
+          nd[q] = right ? pr[q].y : pr[q].x;
+        }
+      }
+    }
+    uint32_t x[ILP], p[ILP];   // node word; its position (slow zero-missing steps only)
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      p[q] = nd[q];
+      base[q] += topb + zfb;   // the bottom: u32 words by position
+      x[q] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+          static_cast<uintptr_t>(base[q] + 4u * nd[q]));
+    }
+    for (;;) {
+      // a leaf's rank is 0xFFFF or 0: x + 0x10000 < 0x20000
+      uint32_t any = 0u;
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) any |= x[q] + 0x10000u;
+      if (__ballot((any & 0xFFFE0000u) != 0u) == 0) break;   // every lane of every tree at a leaf
+      uint32_t b[ILP];
+      rx_u2_t pr[ILP];
+      uint32_t zb[ILP];
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        b[q] = lds_u16((x[q] & bmask) | lane_off);
+#if TI_TC_BCAST
+        // a finished lane reads the tree's first pair (one broadcast address)
+        // and keeps its leaf word
+        pr[q] = lx_rec(base[q] + ((x[q] + 0x10000u) < 0x20000u ? 0u : ((x[q] & 0x3FCu) << 1)));
+#else
+        pr[q] = lx_rec(base[q] + ((x[q] & 0x3FCu) << 1));
+#endif
+        if (SLOW && ZERO) zb[q] = lds_u8(base[q] - zfb + (p[q] >> 3));
+      }
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+#if TI_TC_BCAST
+        const uint32_t x0 = x[q];
+        const uint32_t p0 = p[q];
+#endif
+        if (!SLOW) {
+          asm("v_cmp_lt_u32_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:WORD_0\n\t"
+              "v_cndmask_b32 %0, %2, %3, vcc"
+              : "+v"(x[q]) : "v"(b[q]), "v"(pr[q].x), "v"(pr[q].y) : "vcc");
+        } else {
+          const bool zf = ZERO && ((zb[q] >> (p[q] & 7u)) & 1u) != 0u;
+          const bool right = t16_right_slow<ZERO>(x[q], b[q] & 0xFFFFu, zf);
+          if (ZERO) p[q] = ((x[q] >> 1) & 0x1FEu) + (right ? 1u : 0u);
+          x[q] = right ? pr[q].y : pr[q].x;
+        }
+#if TI_TC_BCAST
+        if ((x0 + 0x10000u) < 0x20000u) {
+          x[q] = x0;
+          p[q] = p0;
+        }
+#endif
+      }
+    }
+    uint32_t li[ILP];   // the leaf's index in the position tables
+#pragma unroll
+    for (int q = 0; q < ILP; ++q) {
+      const int tq = (j + q) < t1 ? (j + q) : (t1 - 1);
+      li[q] = tx_pos[tq] + ((x[q] >> 1) & 0x1FEu) + ((x[q] >> 16) == 0u ? 1u : 0u);
+    }
+    if (VIS) {
+      t8_flush<ACC, KMAX, ILP>(a, acc, pend, pend_t);   // the previous group's leaves
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        pend[q] = static_cast<const ACC*>(a.tx_vals)[li[q]];
+        pend_t[q] = (j + q) < t1 ? (j + q) : -1;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < ILP; ++q) {
+        const int t = j + q;
+        if (t < t1) {
+          const int64_t lf = a.leaf_base[t] + (int64_t)a.tx_ord[li[q]];
+          if (a.kind == TI_OUTPUT_LEAF) {
+            if (live) static_cast<int32_t*>(a.out)[row * a.n_trees + t] = a.exp_leaf_ids[lf];
+          } else {
+            add_leaf<ACC, KMAX>(acc, static_cast<const ACC*>(a.leaves) + lf * a.leaf_width, 0,
+                                a.leaf_width, a.tree_group[t]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
+__global__ void __launch_bounds__(512) t16explicit_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int PF = 8;   // = kLxPf (host): a stage is at most PF x 16 B x R
+  const int R = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + tid;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  u32x4* stage = reinterpret_cast<u32x4*>(smem + a.stage_off);
+  const uint32_t lane_off = (uint32_t)tid * 4u;
+  rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* sst = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.stage_start));
+  const unsigned char* img = a.trees;
+  const int NS = a.n_stages;
+  auto lo_of = [&](int s) { return tx_off[sst[s]]; };   // trees start 16-byte aligned
+  auto n16_of = [&](int s) { return (int)((tx_off[sst[s + 1]] - tx_off[sst[s]]) >> 4); };
+  u32x4 pf[PF];
+  prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(0)), n16_of(0), tid, R);
+  const bool slow = rx_stage_bins<XT, ZERO, false, false>(flag, a, row0, R, tid, stage);
+  const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
+  ACC acc[KMAX];
+  init_acc(acc, a);
+  ACC pend[ILP];   // the previous group's leaf values
+  int pend_t[ILP];
+#pragma unroll
+  for (int q = 0; q < ILP; ++q) {
+    pend[q] = ACC(0);
+    pend_t[q] = -1;
+  }
+  for (int s = 0; s < NS; ++s) {
+    const int t0 = (int)sst[s], t1 = (int)sst[s + 1];
+    const uint32_t lo = lo_of(s);
+    __syncthreads();   // the previous stage's walk is over
+    commit_u<PF>(pf, stage, n16_of(s), tid, R);
+    __syncthreads();
+    const int sn = s + 1 < NS ? s + 1 : s;
+    prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(sn)), n16_of(sn), tid, R);
+    const uint32_t sbase = (uint32_t)a.stage_off - lo;   // LDS address = sbase + image byte
+    if (slow) {
+      if (vis) t16_stage<ACC, KMAX, ZERO, true, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
+      else t16_stage<ACC, KMAX, ZERO, true, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
+    } else {
+      if (vis) t16_stage<ACC, KMAX, ZERO, false, true, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
+      else t16_stage<ACC, KMAX, ZERO, false, false, ILP>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
     }
   }
   if (vis) t8_flush<ACC, KMAX, ILP>(a, acc, pend, pend_t);

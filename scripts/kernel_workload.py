@@ -43,7 +43,8 @@ def main():
     p.add_argument("--rows", type=int, default=1_000_000)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--trees", type=int, default=0,
-                   help="c2 / c2_hist only: the first N trees (fixed cost vs per-tree cost)")
+                   help="c2 / c2_hist / c3*: the first N trees (fixed cost vs per-tree cost; "
+                        "C3's image against one XCD's 4 MB L2)")
     p.add_argument("--x-buffers", type=int, default=1,
                    help="copies of the batch the launches rotate through (bench.py uses 3 for C2)")
     p.add_argument("--streams", type=int, default=1,
@@ -60,6 +61,10 @@ def main():
         trees, ti = synthetic_complete_trees(bench.N_TREES, bench.DEPTH, F, seed=0,
                                              max_bin=254 if a.workload == "c2_hist" else 0)
         forest = forest_from_raw_trees(trees[:a.trees], ti[:a.trees], F, 0, 0.0, "binary:logistic")
+    elif a.trees and a.workload in ("c3", "c3_f64", "c3_maxbin"):
+        from kfserving_amd.formats import lightgbm_format as lf
+        gen = lf.synthetic_maxbin_trees if a.workload == "c3_maxbin" else lf.synthetic_leafwise_trees
+        forest = bench._lgb_forest(gen(1000, 255, 100, seed=1)[:a.trees], "first trees")[0]
     dev = DeviceForest(forest, [0])
     Xs = [bench.device_normal(a.rows, F, 3, "cuda:0", dtype)]
     Xs += [Xs[0].clone() for _ in range(max(0, a.x_buffers - 1))]

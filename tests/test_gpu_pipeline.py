@@ -52,3 +52,27 @@ def test_chunked_host_predict_bit_exact(small_chunks):
     np.testing.assert_allclose(prob, 1 / (1 + np.exp(-got.astype(np.float64))), rtol=1e-5)
     # twice: the lanes' buffers are reused
     assert np.array_equal(dev.predict(X, OUT_MARGIN), got)
+
+
+@pytest.mark.parametrize("strided", [False, True])
+def test_registered_host_predict_bit_exact(small_chunks, strided, monkeypatch):
+    """TI_HOST_REGISTER=1: the caller's X and out page-locked for the call,
+    chunks copied straight from / into them (predict_registered), the same
+    bits as the pinned-chunk pipeline; a row stride and a ragged last chunk."""
+    trees, ti = synthetic_complete_trees(100, 8, 28, seed=4)
+    f = forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic")
+    dev = DeviceForest(f, [0])
+    rows = 40_001
+    W = np.random.default_rng(7).standard_normal((rows, 32 if strided else 28)).astype(np.float32)
+    X = W[:, :28]
+    want = port.xgb_predict(trees, ti, 1, 0.0, 28, np.ascontiguousarray(X))[:, 0]
+    monkeypatch.setenv("TI_HOST_REGISTER", "1")
+    lib, ptr = dev._lib, lambda a: a.ctypes.data
+    out = np.empty(rows, dtype=np.float32)
+    rc = lib.ti_predict(dev._handle, ptr(W), TI_F32, rows, 28, W.shape[1], OUT_MARGIN, ptr(out), rows)
+    assert rc == 0
+    assert np.array_equal(out, want)
+    assert np.array_equal(dev.predict(np.ascontiguousarray(X), OUT_MARGIN), want)   # reused lanes
+    leaf = dev.predict(np.ascontiguousarray(X), OUT_LEAF)
+    monkeypatch.setenv("TI_HOST_REGISTER", "0")
+    assert np.array_equal(leaf, dev.predict(np.ascontiguousarray(X), OUT_LEAF))
