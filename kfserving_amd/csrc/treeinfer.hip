@@ -1451,9 +1451,12 @@ void pack_htop(const ti_forest_desc* d, const std::vector<uint32_t>& slot_of, in
 // carry and what leaves the bin image room in 160 KB).  Falls back to layout 6
 // (returns false) when even ILP tops do not fit.
 constexpr int kHxMinDepth = 12;
+// layout 8's top depth for a forest of depth D (TI_HX_TOP, default 8)
+int hx_top_depth(int D) {
+  return std::max(1, std::min(env_int("TI_HX_TOP", 8), std::min(D, 12)));
+}
 bool plan_htop(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>& slot_of, int D) {
-  int D0 = env_int("TI_HX_TOP", 8);
-  D0 = std::max(1, std::min(D0, std::min(D, 12)));
+  const int D0 = hx_top_depth(D);
   const int ilp = env_int("TI_HX_ILP", 8) >= 8 ? 8 : 4;
   const int R = f->rx[0].rows;
   if (f->rx[1].rows != R) return false;
@@ -1633,7 +1636,10 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
     bmask16 = wmask16 | 2u;
   }
   const uint32_t zfb = (b16 && f->zero_rule) ? ti::kT16ZfBytes : 0u;
-  int D0 = env_int("TI_TX_TOP", 6);
+  // per-lane progress (t16lane_predict_kernel, b16 only): no heap top,
+  // stages of at most kLaneTrees trees
+  const bool lane = b16 && env_int("TI_TX16_PERLANE", 0) != 0;
+  int D0 = lane ? 0 : env_int("TI_TX_TOP", b16 ? 8 : 6);
   // (the u16 bottom also runs without a top: D0 = 0, the root the only entry)
   D0 = std::max(b16 ? 0 : 1, std::min(D0, std::min(D, 10)));
   const int T = d->n_trees;
@@ -1712,16 +1718,21 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
   // 4.70 ms, 7 5.29, 8 5.72 (profiles/r3_tx8_sweep.jsonl)
   const int force_ilp = env_int("TI_LX_ILP", 0);
   int ilp = force_ilp > 0 ? (force_ilp >= 8 ? 8 : force_ilp == 7 ? 7 : 4) : 4;
-  if (b16) {   // the u16 kernel is instantiated at 4, 8, 12 and 16 trees a lane
-    const int i16 = env_int("TI_TX16_ILP", 8);
-    ilp = i16 >= 16 ? 16 : i16 >= 12 ? 12 : i16 >= 8 ? 8 : 4;
+  if (b16) {   // the u16 kernel is instantiated at 4 and 8 trees a lane
+    // (C3 at 1M rows, profiles/r5f_c3_t16_sweep.jsonl: 8 trees a lane and a
+    // top of 8 levels 5.25-5.28 ms; 12 or 16 a lane 5.37-10.9 ms)
+    ilp = env_int("TI_TX16_ILP", 8) >= 8 ? 8 : 4;
   }
   std::vector<int32_t> stages(1, 0);
   int t0 = 0;
   while (t0 < T) {
     int t1 = t0 + 1;
     while (t1 < T && off[t1 + 1] - off[t0] <= cap) ++t1;
-    if (t1 < T && t1 - t0 > ilp) t1 = t0 + ((t1 - t0) / ilp) * ilp;
+    if (lane) {
+      t1 = std::min(t1, t0 + ti::kLaneTrees);
+    } else if (t1 < T && t1 - t0 > ilp) {
+      t1 = t0 + ((t1 - t0) / ilp) * ilp;
+    }
     stages.push_back(t1);
     t0 = t1;
   }
@@ -1808,7 +1819,7 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
   f->lx_stage_cap = static_cast<int64_t>(cap);
   f->lx_ilp = ilp;
   f->hx_top = D0;
-  f->tx8 = b16 ? 2 : 1;
+  f->tx8 = lane ? 3 : b16 ? 2 : 1;
   f->tx16_mask = bmask16;
   f->layout = 9;
   return true;
@@ -2104,6 +2115,13 @@ KernelFn select_t16explicit(int xdt, int accum, int K, bool z, int ilp) {   // l
   return ti::kernels_df(12, K, true, z, true, ilp);
 }
 
+KernelFn select_t16lane(int xdt, int accum, int K, bool z) {   // layout 9, u16, per-lane progress
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(13, K, true, z, true, 0);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(13, K, true, z, true, 0);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(13, K, true, z, true, 0);
+  return ti::kernels_df(13, K, true, z, true, 0);
+}
+
 KernelFn select_hexplicit(int xdt, int accum, int K, bool z, int ilp) {
   if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(8, K, true, z, true, ilp);
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(8, K, true, z, true, ilp);
@@ -2396,7 +2414,8 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.tx_vals = d.tx8_val;
     a.tx_ord = d.tx8_ord;
     a.bin_mask = f->tx16_mask;
-    KernelFn fn = f->tx8 == 2 ? select_t16explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
+    KernelFn fn = f->tx8 == 3 ? select_t16lane(xdt, f->accum, f->K, f->zero_rule != 0)
+                : f->tx8 == 2 ? select_t16explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
                 : f->tx8 ? select_t8explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
                          : select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp, rx.b8 != 0);
     int rc = ensure_lds_attr(d.device, fn);
