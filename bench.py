@@ -270,18 +270,15 @@ def batch_latency_events(launch, n_str, strs, steps, dev_sync):
 
 
 def cpu_baseline(trees, ti, X_host, target_s):
+    """C2 on the host: the port timed on about target_s seconds of rows (the
+    batch tiled when that is more than its 1M rows)."""
     from oracle import port
     n_thr = baseline_threads()
-    probe = min(20_000, X_host.shape[0])
-    t0 = time.perf_counter()
-    port.xgb_predict(trees, ti, 1, 0.0, N_FEAT, X_host[:probe], sigmoid=True, nthread=n_thr)
-    rate = probe / max(time.perf_counter() - t0, 1e-9)
-    n = int(min(X_host.shape[0], max(probe, rate * target_s)))
-    t0 = time.perf_counter()
-    port.xgb_predict(trees, ti, 1, 0.0, N_FEAT, X_host[:n], sigmoid=True, nthread=n_thr)
-    dt = time.perf_counter() - t0
+    n, dt = _scaled_sample(
+        lambda Xs: port.xgb_predict(trees, ti, 1, 0.0, N_FEAT, Xs, sigmoid=True, nthread=n_thr),
+        sample_taker(X_host), target_s)
     return {"value": n / dt, "unit": "rows/s", "cores": n_thr, "kind": "port",
-            "sample": f"{n} rows of the same 1M x 28 batch, oracle/c/tree_port.c "
+            "sample": f"{n} rows of the same 1M x 28 batch (tiled past 1M), oracle/c/tree_port.c "
                       f"(xgboost 0.82 predict loop restated, OpenMP {n_thr} threads), "
                       f"{dt:.1f} s"}
 
