@@ -146,6 +146,9 @@ def parse_args(argv=None):
                         "exceeds the 256 MB Infinity Cache)")
     p.add_argument("--host-rows", type=int, default=8_000_000,
                    help="rows of the host-to-host (PCIe-inclusive) C2 leg (0 = skip)")
+    p.add_argument("--no-tree-shard", action="store_true",
+                   help="skip the tree-sharded C2 leg (every rank a slice of the trees, "
+                        "partial margins summed by one reduce: RCCL over xGMI at N > 1)")
     p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                    help="cpu: the rank logic only, over gloo, with --engine's stand-in "
                         "(tests/test_bench_ranks.py)")
@@ -583,6 +586,60 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
             "_lat_ms": lat_ms}
 
 
+def tree_shard_leg(forest, dev, rows, args, world, rank, local_rank, device, dev_sync,
+                   make_engine=None):
+    """SURVEY 8(e)'s alternative sharding on C2: every rank holds a contiguous
+    slice of the 500 trees (kfserving_amd.tree_shard), all ranks predict the
+    same 1M rows, the partial margins meet in one dist.reduce(SUM) on rank 0
+    (RCCL over xGMI with the nccl backend: rows x 4 B) and rank 0 applies the
+    sigmoid on the device.  K steps, barrier-bracketed, max over ranks;
+    rank 0 checks the result against the replicated forest's predict of the
+    same rows (north_star: 1e-5 relative; bit-identical at N = 1)."""
+    import torch
+    from kfserving_amd.forest import OUT_PREDICT, TI_F32
+    from kfserving_amd.tree_shard import TreeShardedForest
+    factory = None
+    if make_engine is not None:
+        factory = lambda f, d: make_engine(f)            # noqa: E731
+    ts = TreeShardedForest(forest, device=local_rank if device != "cpu" else None,
+                           engine_factory=factory)
+    X = device_normal(rows, N_FEAT, 5, device)           # the same batch on every rank
+    out = [None]
+
+    def step():
+        out[0] = ts.predict(X, OUT_PREDICT)
+
+    step()
+    ev = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          if device != "cpu" else None)
+    wall, _ = timed_steps(step, args.steps, dev_sync, ev)
+    wall = max_over_ranks(wall, device)
+    res = None
+    if rank == 0:
+        t0, t1 = ts.ranges[0]
+        res = {"rows": rows, "ranks": world, "trees_rank0": t1 - t0, "steps": args.steps,
+               "ms_per_step": wall / args.steps * 1e3, "rows_per_s": rows * args.steps / wall,
+               "reduce_bytes": rows * 4 * forest.n_groups if world > 1 else 0,
+               "collective": "dist.reduce(SUM) of [rows, K] float32 partial margins to rank 0"
+                             if world > 1 else "none (one rank)",
+               "path": "kfserving_amd.tree_shard.TreeShardedForest"}
+        if device != "cpu":
+            ref = torch.empty(rows, dtype=torch.float32, device=device)
+            dev.predict_device(X.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
+                               ref.data_ptr(), rows, slot=0,
+                               stream=torch.cuda.current_stream().cuda_stream)
+            dev_sync()
+            got = out[0].reshape(-1).double()
+            want = ref.double()
+            rel = ((got - want).abs() / want.abs().clamp_min(1e-30)).max().item()
+            res["max_rel_diff_vs_replicated"] = rel
+            res["bit_identical"] = bool(torch.equal(out[0].reshape(-1), ref))
+            res["within_1e-5"] = rel <= 1e-5
+    ts.engine.close()
+    del X
+    return res
+
+
 def pool_latency(mine: dict, world: int, rank: int, device):
     """The C5 leg over all ranks: every rank's request latencies gathered to
     rank 0 (all_gather_object, outside any timed region) and the percentiles
@@ -1000,6 +1057,11 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
                        "rows_per_s": rows / (nms * 1e-3)}
         del Xn
 
+    tree_shard = None
+    if not args.no_tree_shard:
+        tree_shard = tree_shard_leg(forest, dev, rows, args, world, rank, local_rank, device,
+                                    dev_sync, make_engine if device == "cpu" else None)
+
     host_pipeline = None
     if args.host_rows > 0 and rank == 0 and device != "cpu":
         host_pipeline = host_to_host(dev, X_host, args.host_rows)
@@ -1089,6 +1151,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             "batched_latency": latency,
             "nan_variant": nan_variant,
             "host_pipeline": host_pipeline,
+            "tree_shard": tree_shard,
         }
         line.update(configs)
     return line

@@ -77,6 +77,10 @@ class TreeShardedForest:
         self.engine = engine_factory(self.local_forest, device)
 
     # ------------------------------------------------------------------
+    def _gloo(self) -> bool:
+        import torch.distributed as dist
+        return dist.get_backend(self.group) == "gloo"
+
     def _dtype(self, kind: int):
         import torch
         if kind == OUT_LEAF:
@@ -104,7 +108,14 @@ class TreeShardedForest:
         self.engine.predict_device(X.data_ptr(), xdt, rows, cols, cols, part_kind,
                                    part.data_ptr(), part.numel(), stream=stream)
         if self.world > 1:
-            dist.reduce(part, dst=self.root, op=dist.ReduceOp.SUM, group=self.group)
+            if part.is_cuda and self._gloo():
+                # gloo reduces host tensors only (a CPU test rig of the RCCL path)
+                host = part.cpu()
+                dist.reduce(host, dst=self.root, op=dist.ReduceOp.SUM, group=self.group)
+                if self.rank == self.root:
+                    part.copy_(host)
+            else:
+                dist.reduce(part, dst=self.root, op=dist.ReduceOp.SUM, group=self.group)
         if self.rank != self.root:
             return None
         if kind != OUT_PREDICT:
@@ -127,8 +138,13 @@ class TreeShardedForest:
         local[:, :t1 - t0] = mine
         if self.world == 1:
             return mine
-        bufs = [torch.empty_like(local) for _ in range(self.world)]
-        dist.all_gather(bufs, local, group=self.group)
+        if local.is_cuda and self._gloo():   # gloo gathers host tensors only
+            bufs = [torch.empty_like(local, device="cpu") for _ in range(self.world)]
+            dist.all_gather(bufs, local.cpu(), group=self.group)
+            bufs = [b.to(X.device) for b in bufs]
+        else:
+            bufs = [torch.empty_like(local) for _ in range(self.world)]
+            dist.all_gather(bufs, local, group=self.group)
         if self.rank != self.root:
             return None
         return torch.cat([bufs[r][:, :b - a] for r, (a, b) in enumerate(self.ranges)], dim=1)

@@ -23,6 +23,9 @@ class StubEngine:
         time.sleep(0.001)
         return np.zeros(np.asarray(X).shape[0], dtype=np.float32)
 
+    def transform_device(self, margin_ptr, n_rows, out_ptr, out_len, slot=0, stream=0):
+        pass
+
     def info(self):
         return {"layout": 3}
 

@@ -35,6 +35,9 @@ class StubEngine:
         self.calls.append((n_rows, n_cols))
         time.sleep(0.02 if self.rank == 1 else 0.001)
 
+    def transform_device(self, margin_ptr, n_rows, out_ptr, out_len, slot=0, stream=0):
+        pass
+
     def info(self):
         return {"layout": 3}
 
@@ -83,8 +86,13 @@ def test_bench_rank_path_two_ranks():
     # stand-in engine writes no outputs, so there is nothing to compare
     assert line["config"]["streams"] == 1 and line["streams_outputs_identical"] is None
     assert line["single_stream"]["value"] == line["value"]
+    # the tree-sharded leg: every rank predicts all 4096 rows over its slice
+    # (1 untimed + 5 timed steps), the partial margins reduced to rank 0
+    assert calls0[1] == [(4096, 28)] * 6 and calls1[1] == [(4096, 28)] * 6
+    ts = line["tree_shard"]
+    assert ts["ranks"] == 2 and ts["rows"] == 4096 and ts["ms_per_step"] >= 20.0
     # C3: strong scaling, 500 rows per rank, 1 untimed + 2 timed steps
-    assert calls0[1] == [(500, 100)] * 3 and calls1[1] == [(500, 100)] * 3
+    assert calls0[2] == [(500, 100)] * 3 and calls1[2] == [(500, 100)] * 3
     c3 = line["c3"]
     assert c3["rows"] == 1000 and c3["rows_per_gpu"] == 500 and c3["scaling"] == "strong"
     assert c3["ms_per_step"] >= 20.0
@@ -130,6 +138,10 @@ def test_bench_cli_gpus_n_starts_n_ranks():
     assert bl["qps_offered"] == 2 * bl["qps_offered_per_gpu"] == 400
     assert bl["p50_ms"] <= bl["p99_ms"] <= bl["max_ms"] and bl["requests"] > 0
     assert "_lat_ms" not in bl
+    # the tree-sharded leg (a reduce over the ranks) is in the line
+    ts = line["tree_shard"]
+    assert ts["ranks"] == 2 and ts["reduce_bytes"] == 2048 * 4 and ts["rows_per_s"] > 0
+    assert 0 < ts["trees_rank0"] < 500
 
 
 def test_headline_defaults_two_streams():

@@ -55,3 +55,9 @@ def test_two_ranks_one_gpu_gloo():
     c3 = line["c3"]
     assert c3["rows"] == 200000 and c3["rows_per_gpu"] == 100000 and c3["scaling"] == "strong"
     assert c3["layout"] == "texplicit"
+    # the tree-sharded leg with the real engine: each rank half the trees, the
+    # partial margins reduced to rank 0 (over the host with gloo here; RCCL on
+    # a node), within north_star's 1e-5 of the replicated forest's predict
+    ts = line["tree_shard"]
+    assert ts["ranks"] == 2 and ts["rows"] == 65536 and 0 < ts["trees_rank0"] < 500
+    assert ts["within_1e-5"], ts
