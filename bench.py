@@ -39,7 +39,8 @@ Also reported (rank 0):
                   array and TD cycles of a committed PMC pass, priced on that
                   pass's own cycles.  C4's cpu_baseline is sklearn's own
                   RandomForestRegressor.predict (kind "library").
-  batched_latency, nan_variant -- see the functions below.
+  batched_latency (native batcher), batched_latency_asyncio, nan_variant --
+  see the functions below.
 """
 from __future__ import annotations
 
@@ -586,6 +587,63 @@ def batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5
             "_lat_ms": lat_ms}
 
 
+def native_batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_latency_ms=5,
+                           seed=7):
+    """The C5 leg through the native batcher (include/kfbatch.h): the same
+    open-loop Poisson arrivals of U{1..64}-row float32 requests as
+    batched_latency, submitted at their scheduled times by a native thread
+    (kb_loadgen: a timed sleep, then a spin), batched in C++ with pkg/batcher
+    semantics and handed straight to ti_predict on host buffers.  Latency =
+    completion (CLOCK_MONOTONIC, stamped when the request's rows are written)
+    - scheduled arrival.  Every request's outputs are then compared with one
+    direct predict of the rows it sent."""
+    from kfserving_amd.batcher.native import NativeBatcher
+    from kfserving_amd.forest import OUT_PREDICT
+    rng = np.random.default_rng(seed)
+    warm = int(qps * 0.5)                 # first 0.5 s of load is warmup, not reported
+    n_req = int(qps * seconds) + warm
+    gaps = rng.exponential(1.0 / qps, n_req)
+    sizes = rng.integers(1, 65, n_req).astype(np.int32)
+    pool = np.random.default_rng(seed + 1).standard_normal((64 * 1024, n_feat), dtype=np.float32)
+    if hasattr(dev, "_handle") and hasattr(dev, "_lib"):
+        nb = NativeBatcher.for_device_forest(dev, max_batch, max_latency_ms, kind=OUT_PREDICT)
+    else:   # a stand-in engine (tests/bench_stub.py): its predict behind the same batcher
+        def call(X, out):
+            out[...] = np.asarray(dev.predict(X, OUT_PREDICT)).reshape(out.shape)
+            return 0
+        nb = NativeBatcher(call, n_feat, 0, 1, np.float32, max_batch, max_latency_ms)
+    dev.predict(pool[:4096], OUT_PREDICT)
+    arrivals = np.cumsum(gaps)
+    lat, st, out, t0 = nb.loadgen(arrivals, sizes, pool)
+    stats = nb.stats()
+    nb.close()
+    want = np.asarray(dev.predict(pool, OUT_PREDICT)).reshape(-1)
+    ok = bool((st == 0).all())
+    for i in range(n_req):
+        off = (i * 64) % (pool.shape[0] - 64)
+        s = int(sizes[i])
+        if not np.array_equal(out[i * 64:i * 64 + s], want[off:off + s]):
+            ok = False
+            break
+    lat_ms = lat[warm:]
+    wall = (arrivals[-1] + lat[-1] * 1e-3)   # first arrival at t0 .. last completion
+    nb_ = max(1, stats["batches"])
+    return {"qps_offered": qps, "requests": n_req - warm, "rows_per_request": "U{1..64}",
+            "max_batch_size": max_batch, "max_latency_ms": max_latency_ms,
+            "p50_ms": float(np.percentile(lat_ms, 50)), "p99_ms": float(np.percentile(lat_ms, 99)),
+            "max_ms": float(lat_ms.max()), "rows_per_s": float(sizes.sum() / wall),
+            "p90_ms": float(np.percentile(lat_ms, 90)),
+            "p999_ms": float(np.percentile(lat_ms, 99.9)),
+            "batches": int(stats["batches"]), "mean_batch_rows": stats["rows"] / nb_,
+            "timer_flushes": int(stats["timer_flushes"]), "full_flushes": int(stats["full_flushes"]),
+            "model_ms_mean": stats["model_ms_total"] / nb_,
+            "outputs_match_direct_predict": ok,
+            "path": "native batcher (libkfserve kb_*, pkg/batcher semantics) -> ti_predict "
+                    "(host buffers), arrivals submitted by a native thread (kb_loadgen), 1 GPU, "
+                    "no HTTP/JSON",
+            "_lat_ms": lat_ms}
+
+
 def tree_shard_leg(forest, dev, rows, args, world, rank, local_rank, device, dev_sync,
                    make_engine=None):
     """SURVEY 8(e)'s alternative sharding on C2: every rank holds a contiguous
@@ -651,7 +709,8 @@ def pool_latency(mine: dict, world: int, rank: int, device):
         mine.update(devices=1, qps_offered_per_gpu=mine["qps_offered"])
         return mine
     got = [None] * world
-    dist.all_gather_object(got, (lat, mine["rows_per_s"], mine["p99_ms"], mine["batches"]))
+    dist.all_gather_object(got, (lat, mine["rows_per_s"], mine["p99_ms"], mine["batches"],
+                                 mine.get("outputs_match_direct_predict")))
     if rank != 0:
         return None
     allm = np.concatenate([g[0] for g in got])
@@ -663,9 +722,10 @@ def pool_latency(mine: dict, world: int, rank: int, device):
                max_ms=float(allm.max()), rows_per_s=float(sum(g[1] for g in got)),
                p99_ms_per_rank=[float(g[2]) for g in got],
                batches=int(sum(g[3] for g in got)),
-               path=f"{world} ranks, each an in-process batcher -> ti_predict (host buffers) "
-                    "on its own GPU, no HTTP/JSON; percentiles over all ranks' requests "
-                    "(rank 0's batch statistics and worst request)")
+               **({"outputs_match_direct_predict": all(g[4] for g in got)}
+                  if "outputs_match_direct_predict" in mine else {}),
+               path=f"{world} ranks, each on its own GPU: {mine['path']}; percentiles over "
+                    "all ranks' requests (rank 0's batch statistics)")
     return out
 
 
@@ -1022,16 +1082,22 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
     # that load the host (CPU baselines' thread pools, the 8M-row host
     # pipeline) or hold tens of GB on the device (C3 / C4): its p99 then
     # measures the batcher and the engine, not what ran before it
-    latency = None
+    latency = latency_asyncio = None
     if args.latency_qps > 0:
         # C5 on every GPU at once: each rank is one serving worker with its own
         # batcher in front of its own GPU (KFServer's pre-forked workers, one
         # GPU each), offered latency_qps; the latencies of all ranks are
         # pooled on rank 0
         barrier_sync(dev_sync)
+        mine = native_batched_latency(dev, N_FEAT, args.latency_qps, args.latency_seconds,
+                                      seed=7 + 1000 * rank)
+        latency = pool_latency(mine, world, rank, device)
+        # the same load through the asyncio batcher (kfserving_amd.batcher.Batcher,
+        # KF_NATIVE_BATCHER=0), for comparison
+        barrier_sync(dev_sync)
         mine = batched_latency(dev, N_FEAT, args.latency_qps, args.latency_seconds,
                                seed=7 + 1000 * rank)
-        latency = pool_latency(mine, world, rank, device)
+        latency_asyncio = pool_latency(mine, world, rank, device)
 
     nan_variant = None
     if args.nan_variant > 0 and rank == 0 and device != "cpu":
@@ -1149,6 +1215,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
                                           two_stream, n_str),
             "cpu_baseline": cpu,
             "batched_latency": latency,
+            "batched_latency_asyncio": latency_asyncio,
             "nan_variant": nan_variant,
             "host_pipeline": host_pipeline,
             "tree_shard": tree_shard,

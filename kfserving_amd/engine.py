@@ -168,6 +168,22 @@ def default_devices() -> Sequence[int]:
     return list(range(device_count()))
 
 
+def prepare_input(forest: Forest, X) -> np.ndarray:
+    """Convert X the way the library being replaced converts it.
+
+    XGBoost's DMatrix and sklearn's check_array make float32; LightGBM
+    keeps float32 input as float32 and reads anything else as float64.
+    """
+    X = np.asarray(X)
+    if X.ndim == 1:
+        X = X.reshape(1, -1)
+    if X.ndim != 2:
+        raise ValueError(f"expected a 2-D input, got shape {X.shape}")
+    if forest.input_dtype == TI_F64 and X.dtype != np.float32:
+        return np.ascontiguousarray(X, dtype=np.float64)
+    return np.ascontiguousarray(X, dtype=np.float32)
+
+
 def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
@@ -240,19 +256,7 @@ class DeviceForest:
 
     # --------------------------------------------------------------- predict
     def prepare_input(self, X) -> np.ndarray:
-        """Convert X the way the library being replaced converts it.
-
-        XGBoost's DMatrix and sklearn's check_array make float32; LightGBM
-        keeps float32 input as float32 and reads anything else as float64.
-        """
-        X = np.asarray(X)
-        if X.ndim == 1:
-            X = X.reshape(1, -1)
-        if X.ndim != 2:
-            raise ValueError(f"expected a 2-D input, got shape {X.shape}")
-        if self.forest.input_dtype == TI_F64 and X.dtype != np.float32:
-            return np.ascontiguousarray(X, dtype=np.float64)
-        return np.ascontiguousarray(X, dtype=np.float32)
+        return prepare_input(self.forest, X)
 
     def predict(self, X, kind: int = OUT_PREDICT) -> np.ndarray:
         X = self.prepare_input(X)
@@ -294,7 +298,7 @@ class DeviceForest:
             pass
 
 
-__all__ = ["DeviceForest", "TreeInferError", "load_library", "device_count", "default_devices",
+__all__ = ["DeviceForest", "TreeInferError", "prepare_input", "load_library", "device_count", "default_devices",
            "OPT_SHAP_TABLE_ROWS", "OPT_SHAP_TABLE_MB",
            "EXPORTED_SYMBOLS", "OUT_MARGIN", "OUT_PREDICT", "OUT_LEAF", "OUT_CONTRIB", "TI_F32", "TI_F64",
            "TI_I32"]

@@ -460,9 +460,15 @@ class KFServer:
         factory = None
         if self.max_batchsize and self.max_batchsize > 0:
             from ..batcher.batcher import ModelBatcher
+            from ..batcher.native import NativeModelBatcher, native_batching_enabled
             size, lat = self.max_batchsize, self.max_latency_ms
 
             def factory(model, call, kind="instances"):
+                # the GPU tree plugins batch in native code (kfbatch.h); any
+                # other KFModel keeps the asyncio batcher
+                if native_batching_enabled(model):
+                    return NativeModelBatcher(model, kind=kind, max_batch_size=size,
+                                              max_latency_ms=lat)
                 return ModelBatcher(model, call, kind=kind, max_batch_size=size,
                                     max_latency_ms=lat)
         return Application(self.registered_models, batcher_factory=factory,

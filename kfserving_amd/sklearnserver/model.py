@@ -15,6 +15,7 @@ import numpy as np
 from ..formats.sklearn_format import forest_from_sklearn, load_tree_arrays
 from ..kfserving.kfmodel import KFModel
 from ..kfserving.storage import Storage
+from ..engine import prepare_input
 from ..tree_model import GPUForestMixin
 
 MODEL_BASENAME = "model"
@@ -81,6 +82,17 @@ class SKLearnModel(GPUForestMixin, KFModel):  # pylint:disable=c-extension-no-me
         if classes is not None:
             result = np.asarray(classes).take(result.astype(np.int64), axis=0)
         return result
+
+    def native_rows(self, chunk, kind: str) -> np.ndarray:
+        # the same checks for V2 tensors and instances (predict_tensor)
+        X = chunk if kind == "inputs" else self.request_matrix({"instances": chunk})
+        return prepare_input(self._forest, X)
+
+    def native_predictions(self, out: np.ndarray, kind: str):
+        classes = self._forest.meta.get("classes")
+        if classes is not None:
+            out = np.asarray(classes).take(out.astype(np.int64), axis=0)
+        return out if kind == "tensor" else out.tolist()
 
     def predict(self, request: Dict) -> Dict:
         inputs = self._array(request)

@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-from .engine import DeviceForest
+from .engine import DeviceForest, prepare_input
 from .forest import OUT_CONTRIB, OUT_PREDICT, Forest
 
 
@@ -63,6 +63,24 @@ class GPUForestMixin:
             return {"predictions": self.predict_tensor(X)}
         except Exception as e:
             raise Exception("Failed to predict %s" % e)
+
+    # KFServer's native batcher (kfserving_amd.batcher.native.NativeModelBatcher):
+    # each request is converted here exactly as predict / predict_batched /
+    # predict_tensor convert it, and its rows of the batch's output become its
+    # predictions as those methods return them
+    native_batching = True
+
+    def native_rows(self, chunk, kind: str) -> np.ndarray:
+        if kind == "inputs":          # already batch_inputs' float64 matrix
+            X = chunk
+        elif kind == "tensor":
+            X = self.tensor_matrix(chunk)
+        else:
+            X = self.request_matrix({"instances": chunk})
+        return prepare_input(self._forest, X)
+
+    def native_predictions(self, out: np.ndarray, kind: str):
+        return out if kind == "tensor" else out.tolist()
 
     def explain(self, request: Dict) -> Dict:
         """The ``:explain`` route (kfserver.py:79-82 in the reference, which

@@ -138,6 +138,11 @@ def test_bench_cli_gpus_n_starts_n_ranks():
     assert bl["qps_offered"] == 2 * bl["qps_offered_per_gpu"] == 400
     assert bl["p50_ms"] <= bl["p99_ms"] <= bl["max_ms"] and bl["requests"] > 0
     assert "_lat_ms" not in bl
+    # the leg runs through the native batcher, every request's rows checked
+    # against a direct predict; the asyncio batcher's run is beside it
+    assert "native batcher" in bl["path"] and bl["outputs_match_direct_predict"] is True
+    ba = line["batched_latency_asyncio"]
+    assert ba["devices"] == 2 and ba["requests"] == bl["requests"] and "_lat_ms" not in ba
     # the tree-sharded leg (a reduce over the ranks) is in the line
     ts = line["tree_shard"]
     assert ts["ranks"] == 2 and ts["reduce_bytes"] == 2048 * 4 and ts["rows_per_s"] > 0

@@ -1,0 +1,264 @@
+"""The native batcher (include/kfbatch.h, libkfserve.so) against pkg/batcher's
+semantics (pkg/batcher/handler.go:98-263), CPU only: the model call is a
+Python function behind the same ti_predict-shaped pointer, so the C++ flush,
+fan-out, failure and shutdown logic runs exactly as it does in front of
+libtreeinfer.  The -m gpu twin is tests/test_gpu_native_batcher.py."""
+import asyncio
+import ctypes
+import os
+import re
+import subprocess
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from kfserving_amd.batcher.native import (BatchError, EXPORTED_SYMBOLS, KbCompletion, KbConfig,
+                                          KbStats, NativeBatcher, load_library)
+from kfserving_amd.forest import TI_F32, TI_F64
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+def sum_batcher(max_batch_size=32, max_latency_ms=50, width=1, x_dtype=TI_F32, fail=None,
+                delay=0.0, **kw):
+    """A batcher whose model writes each row's sum (times 1..width) and logs
+    every call's row count."""
+    calls = []
+    lock = threading.Lock()
+
+    def model(X, out):
+        with lock:
+            calls.append(X.shape[0])
+        if delay:
+            time.sleep(delay)
+        if fail is not None:
+            raise ValueError(fail)
+        s = X.astype(np.float64).sum(axis=1)
+        if width == 1:
+            out[:] = s
+        else:
+            out[:] = s[:, None] * np.arange(1, width + 1)
+        return 0
+    odt = np.float32 if x_dtype == TI_F32 else np.float64
+    b = NativeBatcher(model, 3, x_dtype, width, odt, max_batch_size, max_latency_ms, **kw)
+    return b, calls
+
+
+def rows(n, seed, dt=np.float32):
+    return np.random.default_rng(seed).standard_normal((n, 3)).astype(dt)
+
+
+def test_header_declares_the_binding_symbols():
+    src = open(os.path.join(ROOT, "include", "kfbatch.h")).read()
+    names = sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t)\s+(kb_\w+)\(", src, re.M)))
+    assert names == sorted(EXPORTED_SYMBOLS)
+    lib = load_library()
+    out = subprocess.run(["nm", "-D", "--defined-only", lib._name], capture_output=True,
+                         text=True, check=True).stdout
+    assert set(names) <= set(re.findall(r"\bT (kb_\w+)", out))
+
+
+def test_struct_layout_matches_header(tmp_path):
+    prog = tmp_path / "layout.c"
+    structs = {"kb_config": KbConfig, "kb_completion": KbCompletion, "kb_stats": KbStats}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "kfbatch.h"', 'int main(){']
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        lines += [f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));' for f, _ in py._fields_]
+    lines.append("return 0;}")
+    prog.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)],
+                   check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                  check=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(py, f).offset, (cname, f)
+
+
+def test_flush_on_max_batch_rows_and_fan_out():
+    """handler.go:179: CurrentInputLen >= MaxBatchSize flushes; each request
+    gets its own rows back by index, all with the batch's one batchId."""
+    async def go():
+        b, calls = sum_batcher(max_batch_size=4, max_latency_ms=10_000)
+        xs = [rows(1, 0), rows(2, 1), rows(1, 2)]
+        res = await asyncio.gather(*[b.submit(x) for x in xs])
+        b.close()
+        return xs, res, calls
+    xs, res, calls = run(go())
+    assert calls == [4]
+    ids = {bid for _, bid in res}
+    assert len(ids) == 1 and re.fullmatch(r"[0-9a-f]{8}-[0-9a-f]{4}-4[0-9a-f]{3}-[89ab][0-9a-f]{3}-"
+                                          r"[0-9a-f]{12}", ids.pop())
+    for x, (out, _) in zip(xs, res):
+        np.testing.assert_array_equal(out, x.astype(np.float64).sum(axis=1).astype(np.float32))
+
+
+def test_whole_requests_overshoot_max_batch():
+    """A request is appended whole (handler.go:165-175), so a batch may hold
+    more rows than MaxBatchSize."""
+    async def go():
+        b, calls = sum_batcher(max_batch_size=4, max_latency_ms=10_000)
+        res = await asyncio.gather(b.submit(rows(3, 0)), b.submit(rows(3, 1)))
+        st = b.stats()
+        b.close()
+        return res, calls, st
+    res, calls, st = run(go())
+    assert calls == [6]
+    assert st["full_flushes"] == 1 and st["max_batch_rows"] == 6 and st["rows"] == 6
+    assert [o.shape for o, _ in res] == [(3,), (3,)]
+
+
+def test_flush_on_max_latency():
+    """Now.Sub(Start) >= MaxLatency flushes (handler.go:180), Start being the
+    first request's arrival; one batch for requests inside the window."""
+    async def go():
+        b, calls = sum_batcher(max_batch_size=1000, max_latency_ms=40)
+        t0 = time.monotonic()
+        f1 = b.submit_nowait(rows(2, 0))
+        await asyncio.sleep(0.01)
+        f2 = b.submit_nowait(rows(5, 1))
+        await asyncio.gather(f1, f2)
+        dt = time.monotonic() - t0
+        st = b.stats()
+        b.close()
+        return dt, calls, st
+    dt, calls, st = run(go())
+    assert calls == [7]
+    assert st["timer_flushes"] == 1
+    assert 0.040 <= dt < 0.5
+
+
+def test_deadline_is_precise():
+    """The timer flushes within a fraction of a millisecond of the deadline
+    (CLOCK_MONOTONIC wait; the Go loop polls every 100 us, asyncio's epoll
+    timers round up to whole milliseconds)."""
+    async def go():
+        b, _ = sum_batcher(max_batch_size=10_000, max_latency_ms=3)
+        lates = []
+        for i in range(20):
+            t0 = time.monotonic()
+            await b.submit(rows(1, i))
+            lates.append(time.monotonic() - t0 - 0.003)
+        b.close()
+        return np.array(lates)
+    lates = run(go())
+    assert (lates >= 0).all()
+    assert np.median(lates) < 1e-3
+
+
+def test_model_failure_fans_out_message():
+    """A failed model call fans its message out to every request of the batch
+    (handler.go:107-116)."""
+    async def go():
+        b, calls = sum_batcher(max_batch_size=3, max_latency_ms=10_000, fail="boom 42")
+        res = await asyncio.gather(b.submit(rows(1, 0)), b.submit(rows(2, 1)),
+                                   return_exceptions=True)
+        st = b.stats()
+        b.close()
+        return res, st
+    res, st = run(go())
+    assert all(isinstance(r, BatchError) and "boom 42" in str(r) for r in res)
+    assert st["failed_batches"] == 1
+
+
+def test_batches_pipeline_while_the_model_runs():
+    """With two model threads, the next batch forms and runs while a slow one
+    is on the model (the Go loop would block, handler.go:182)."""
+    async def go(inflight):
+        b, calls = sum_batcher(max_batch_size=2, max_latency_ms=10_000, delay=0.2,
+                               max_inflight=inflight)
+        t0 = time.monotonic()
+        await asyncio.gather(*[b.submit(rows(1, i)) for i in range(4)])
+        dt = time.monotonic() - t0
+        b.close()
+        return dt, calls
+    dt2, calls2 = run(go(2))
+    dt1, calls1 = run(go(1))
+    assert calls2 == [2, 2] and calls1 == [2, 2]
+    assert dt2 < 0.35 <= dt1
+
+
+def test_float64_rows_and_vector_outputs():
+    async def go():
+        b, _ = sum_batcher(max_batch_size=5, max_latency_ms=10_000, width=3, x_dtype=TI_F64)
+        xs = [rows(2, 0, np.float64), rows(3, 1, np.float64)]
+        res = await asyncio.gather(*[b.submit(x) for x in xs])
+        b.close()
+        return xs, res
+    xs, res = run(go())
+    for x, (out, _) in zip(xs, res):
+        assert out.shape == (x.shape[0], 3) and out.dtype == np.float64
+        np.testing.assert_array_equal(out, x.sum(axis=1)[:, None] * np.arange(1, 4))
+
+
+def test_drain_and_close():
+    """drain() flushes what is forming and waits for it; close() after it
+    leaves nothing pending; a closed batcher refuses new requests."""
+    async def go():
+        b, calls = sum_batcher(max_batch_size=1000, max_latency_ms=60_000)
+        f = b.submit_nowait(rows(4, 0))
+        await b.drain()
+        out, _ = f.result()
+        b.close()
+        with pytest.raises(RuntimeError):
+            b.submit_nowait(rows(1, 1))
+        return out, calls
+    out, calls = run(go())
+    assert calls == [4] and out.shape == (4,)
+
+
+def test_bad_requests_rejected():
+    async def go():
+        b, _ = sum_batcher()
+        with pytest.raises(Exception):
+            b.submit_nowait(np.zeros((0, 3), np.float32))
+        with pytest.raises(ValueError):
+            b.submit_nowait(np.zeros((2, 4), np.float32))
+        b.close()
+    run(go())
+
+
+def test_loadgen_open_loop():
+    """kb_loadgen: every request answered with its own rows' outputs, latency
+    from the scheduled arrival, batches flushed by the deadline."""
+    b, calls = sum_batcher(max_batch_size=65536, max_latency_ms=5)
+    rng = np.random.default_rng(3)
+    n = 400
+    arr = np.cumsum(rng.exponential(1 / 2000.0, n))
+    sz = rng.integers(1, 65, n).astype(np.int32)
+    pool = rng.standard_normal((4096, 3)).astype(np.float32)
+    lat, st, out, t0 = b.loadgen(arr, sz, pool)
+    stats = b.stats()
+    b.close()
+    assert (st == 0).all()
+    assert (lat > 0).all() and np.percentile(lat, 50) < 5.0 + 20.0
+    assert stats["rows"] == int(sz.sum()) and stats["timer_flushes"] >= 1
+    for i in range(0, n, 37):
+        off = (i * 64) % (4096 - 64)
+        want = pool[off:off + sz[i]].astype(np.float64).sum(axis=1).astype(np.float32)
+        np.testing.assert_array_equal(out[i * 64:i * 64 + sz[i]], want)
+
+
+def test_server_uses_native_batcher_unless_disabled(monkeypatch, golden, tmp_path):
+    """KFServer --max_batchsize puts the native batcher in front of the GPU tree
+    plugins; KF_NATIVE_BATCHER=0 keeps the asyncio batcher."""
+    from kfserving_amd.batcher.batcher import ModelBatcher
+    from kfserving_amd.batcher.native import NativeModelBatcher
+    from kfserving_amd.kfserving import KFServer
+    from tests.test_lgb_batching import _lgb_model
+    model = _lgb_model(golden, tmp_path)
+    app = KFServer(max_batchsize=8, max_latency_ms=5).create_application()
+    nb = app._batcher_factory(model, app._call, "inputs")
+    assert isinstance(nb, NativeModelBatcher)
+    nb.close()
+    monkeypatch.setenv("KF_NATIVE_BATCHER", "0")
+    assert isinstance(app._batcher_factory(model, app._call, "inputs"), ModelBatcher)
