@@ -114,6 +114,19 @@ int kb_notify_fd(void* batcher);
 int kb_submit(void* batcher, const void* X, int64_t rows, int64_t row_stride, void* out,
               uint64_t tag);
 
+/* kb_submit for a request whose rows are of another element type or still
+ * need the plugin's conversion: each element is converted while it is copied
+ * into the batch (an IEEE cast, numpy's astype), after `transform`:
+ *   KB_IN_PLAIN      the value as it is;
+ *   KB_IN_XGB_LIST   xgboost 0.82's DMatrix(list) (xgbserver/model.py:46): the
+ *                    scipy.sparse conversion keeps no zeros, so 0 is missing
+ *                    (NaN), and a stored NaN never satisfies x < split (+inf).
+ * x_dtype: TI_F32 (0) or TI_F64 (1). */
+#define KB_IN_PLAIN     0
+#define KB_IN_XGB_LIST  1
+int kb_submit_convert(void* batcher, const void* X, int32_t x_dtype, int64_t rows,
+                      int64_t row_stride, int32_t transform, void* out, uint64_t tag);
+
 /* Move up to `cap` completions into `out`; returns how many (0: none). */
 int kb_poll(void* batcher, kb_completion* out, int32_t cap);
 

@@ -31,8 +31,10 @@ from ..kfserving.errors import HTTPError
 
 KB_ABI_VERSION = 1
 KB_OK, KB_ERR_INVALID, KB_ERR_CLOSED, KB_ERR_SYSTEM, KB_ERR_MODEL = 0, -1, -2, -3, -4
+KB_IN_PLAIN, KB_IN_XGB_LIST = 0, 1   # kb_submit_convert transforms
 
-EXPORTED_SYMBOLS = ("kb_create", "kb_destroy", "kb_flush", "kb_notify_fd", "kb_submit", "kb_poll",
+EXPORTED_SYMBOLS = ("kb_create", "kb_destroy", "kb_flush", "kb_notify_fd", "kb_submit",
+                    "kb_submit_convert", "kb_poll",
                     "kb_batch_message", "kb_get_stats", "kb_now_ns", "kb_loadgen",
                     "kb_abi_version")
 
@@ -89,6 +91,8 @@ def load_library() -> ctypes.CDLL:
     lib.kb_notify_fd.argtypes = [vp]
     lib.kb_submit.restype = ctypes.c_int
     lib.kb_submit.argtypes = [vp, vp, i64, i64, vp, u64]
+    lib.kb_submit_convert.restype = ctypes.c_int
+    lib.kb_submit_convert.argtypes = [vp, vp, i32, i64, i64, i32, vp, u64]
     lib.kb_poll.restype = ctypes.c_int
     lib.kb_poll.argtypes = [vp, ctypes.POINTER(KbCompletion), i32]
     lib.kb_batch_message.restype = ctypes.c_int
@@ -196,14 +200,19 @@ class NativeBatcher:
         loop.add_reader(self._fd, self._drain)
         self._loop = loop
 
-    def submit_nowait(self, X: np.ndarray) -> "asyncio.Future":
-        """Queue the rows of X (converted to the batcher's input type); the
-        future resolves to ``(out, batch_id)`` or raises :class:`BatchError`."""
+    def submit_nowait(self, X: np.ndarray, transform: int = KB_IN_PLAIN) -> "asyncio.Future":
+        """Queue the rows of X; the future resolves to ``(out, batch_id)`` or
+        raises :class:`BatchError`.  float32 / float64 rows are converted to
+        the batcher's input type while they are copied (kb_submit_convert),
+        after ``transform`` (KB_IN_XGB_LIST: xgboost's DMatrix(list) rule)."""
         if self._h is None:
             raise RuntimeError("batcher is closed")
         loop = asyncio.get_running_loop()
         self._attach(loop)
-        X = np.ascontiguousarray(X, dtype=self._x_np)
+        X = np.asarray(X)
+        if X.dtype not in (np.float32, np.float64) or X.ndim != 2 or X.strides[1] != X.itemsize \
+                or X.strides[0] % X.itemsize:
+            X = np.ascontiguousarray(X, dtype=self._x_np)
         if X.ndim != 2 or X.shape[0] == 0:
             raise HTTPError(400, "no instances in the request")
         if X.shape[1] != self.n_cols:
@@ -213,14 +222,16 @@ class NativeBatcher:
         tag = next(self._tags)
         fut = loop.create_future()
         self._pending[tag] = (fut, out)
-        rc = self._lib.kb_submit(self._h, X.ctypes.data, rows, self.n_cols, out.ctypes.data, tag)
+        rc = self._lib.kb_submit_convert(self._h, X.ctypes.data, 0 if X.dtype == np.float32 else 1,
+                                         rows, X.strides[0] // X.itemsize, int(transform),
+                                         out.ctypes.data, tag)
         if rc != KB_OK:
             del self._pending[tag]
             raise RuntimeError(f"kb_submit failed ({rc})")
         return fut
 
-    async def submit(self, X: np.ndarray):
-        return await self.submit_nowait(X)
+    async def submit(self, X: np.ndarray, transform: int = KB_IN_PLAIN):
+        return await self.submit_nowait(X, transform)
 
     def _drain(self) -> None:
         try:
@@ -342,7 +353,7 @@ class NativeModelBatcher:
 
     async def submit(self, chunk) -> Dict[str, Any]:
         try:
-            X = self.model.native_rows(chunk, self.kind)
+            X, transform = self.model.native_request(chunk, self.kind)
         except HTTPError:
             raise
         except Exception as e:
@@ -350,7 +361,7 @@ class NativeModelBatcher:
         if X.shape[0] == 0:
             raise HTTPError(400, "no instances in the request")
         try:
-            out, batch_id = await self._nb.submit(X)
+            out, batch_id = await self._nb.submit(X, transform)
         except BatchError as e:
             return {"message": "Failed to predict %s" % e, "batchId": "", "predictions": None}
         return {"message": "", "batchId": batch_id,
@@ -371,4 +382,5 @@ def native_batching_enabled(model) -> bool:
 
 
 __all__ = ["NativeBatcher", "NativeModelBatcher", "BatchError", "load_library", "now_ns",
+           "KB_IN_PLAIN", "KB_IN_XGB_LIST",
            "native_batching_enabled", "EXPORTED_SYMBOLS", "PREDICT_FN", "ERROR_FN"]

@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <limits>
 #include <mutex>
 #include <random>
 #include <string>
@@ -214,6 +215,28 @@ void worker_main(Batcher* bp) {
   }
 }
 
+// one element of a request converted into the batch's type: an IEEE cast
+// (numpy's astype: round to nearest even, overflow to inf), after xgboost
+// 0.82's DMatrix(list) rule when asked (scipy.sparse.csr_matrix keeps no
+// zeros, so 0 is missing = NaN; a NaN it does store compares false with every
+// split, i.e. always goes right = +inf; tree_model.xgb_matrix_from_list)
+template <typename D, typename S>
+inline D convert(S v, int transform) {
+  if (transform == KB_IN_XGB_LIST) {
+    if (v == S(0)) return std::numeric_limits<D>::quiet_NaN();
+    if (v != v) return std::numeric_limits<D>::infinity();
+  }
+  return static_cast<D>(v);
+}
+
+template <typename D, typename S>
+void convert_rows(unsigned char* dst, const S* src, int64_t rows, int64_t stride, int cols,
+                  int transform) {
+  D* d = reinterpret_cast<D*>(dst);
+  for (int64_t r = 0; r < rows; ++r)
+    for (int c = 0; c < cols; ++c) d[r * cols + c] = convert<D, S>(src[r * stride + c], transform);
+}
+
 }  // namespace
 
 extern "C" {
@@ -293,9 +316,19 @@ int kb_notify_fd(void* h) { return h ? static_cast<Batcher*>(h)->efd : KB_ERR_IN
 
 int kb_submit(void* h, const void* X, int64_t rows, int64_t row_stride, void* out,
               uint64_t tag) {
+  if (!h) return KB_ERR_INVALID;
+  return kb_submit_convert(h, X, static_cast<Batcher*>(h)->cfg.x_dtype, rows, row_stride,
+                           KB_IN_PLAIN, out, tag);
+}
+
+int kb_submit_convert(void* h, const void* X, int32_t x_dtype, int64_t rows, int64_t row_stride,
+                      int32_t transform, void* out, uint64_t tag) {
   if (!h || !X || !out || rows <= 0) return KB_ERR_INVALID;
   Batcher& b = *static_cast<Batcher*>(h);
-  if (row_stride < b.cfg.n_cols) return KB_ERR_INVALID;
+  if (row_stride < b.cfg.n_cols || (x_dtype != 0 && x_dtype != 1) ||
+      (transform != KB_IN_PLAIN && transform != KB_IN_XGB_LIST))
+    return KB_ERR_INVALID;
+  const bool copy = x_dtype == b.cfg.x_dtype && transform == KB_IN_PLAIN;
   const size_t es = b.cfg.x_dtype == 0 ? 4 : 8;
   const unsigned char* src = static_cast<const unsigned char*>(X);
   std::unique_lock<std::mutex> lk(b.mu);
@@ -311,7 +344,18 @@ int kb_submit(void* h, const void* X, int64_t rows, int64_t row_stride, void* ou
   }
   const size_t at = f.x.size();
   f.x.resize(at + static_cast<size_t>(rows) * b.x_row);
-  if (row_stride == b.cfg.n_cols) {
+  if (!copy) {
+    unsigned char* dst = f.x.data() + at;
+    const int nc = b.cfg.n_cols;
+    if (b.cfg.x_dtype == 0 && x_dtype == 1)
+      convert_rows<float, double>(dst, static_cast<const double*>(X), rows, row_stride, nc, transform);
+    else if (b.cfg.x_dtype == 0)
+      convert_rows<float, float>(dst, static_cast<const float*>(X), rows, row_stride, nc, transform);
+    else if (x_dtype == 1)
+      convert_rows<double, double>(dst, static_cast<const double*>(X), rows, row_stride, nc, transform);
+    else
+      convert_rows<double, float>(dst, static_cast<const float*>(X), rows, row_stride, nc, transform);
+  } else if (row_stride == b.cfg.n_cols) {
     std::memcpy(f.x.data() + at, src, static_cast<size_t>(rows) * b.x_row);
   } else {
     for (int64_t r = 0; r < rows; ++r)

@@ -79,6 +79,11 @@ class GPUForestMixin:
             X = self.request_matrix({"instances": chunk})
         return prepare_input(self._forest, X)
 
+    def native_request(self, chunk, kind: str):
+        """(matrix, kb_submit_convert transform) for one request: by default
+        the converted rows of native_rows, copied as they are."""
+        return self.native_rows(chunk, kind), 0
+
     def native_predictions(self, out: np.ndarray, kind: str):
         return out if kind == "tensor" else out.tolist()
 

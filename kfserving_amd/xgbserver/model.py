@@ -51,6 +51,15 @@ class XGBoostModel(GPUForestMixin, KFModel):
             X = X.reshape(1, -1)
         return X if X.dtype == np.float32 else X.astype(np.float32)
 
+    def native_request(self, chunk, kind: str):
+        # a natively decoded JSON list: DMatrix(list)'s rule (0 missing, NaN
+        # right) and the float32 cast are applied by the native batcher while
+        # it copies the rows (KB_IN_XGB_LIST), the conversion
+        # xgb_matrix_from_list makes in numpy
+        if kind == "instances" and isinstance(chunk, JsonInstances) and chunk.ndim == 2:
+            return np.asarray(chunk), 1
+        return super().native_request(chunk, kind)
+
     def predict(self, request: Dict) -> Dict:
         try:
             result = self.predict_matrix(self.request_matrix(request))

@@ -262,3 +262,50 @@ def test_server_uses_native_batcher_unless_disabled(monkeypatch, golden, tmp_pat
     nb.close()
     monkeypatch.setenv("KF_NATIVE_BATCHER", "0")
     assert isinstance(app._batcher_factory(model, app._call, "inputs"), ModelBatcher)
+
+
+def identity_batcher(x_dtype):
+    """A model that answers each row with the row itself (3 columns), so the
+    batch's input -- after kb_submit_convert -- comes back bit for bit."""
+    odt = np.float32 if x_dtype == TI_F32 else np.float64
+
+    def model(X, out):
+        out[:] = X
+        return 0
+    return NativeBatcher(model, 3, x_dtype, 3, odt, 1000, 1)
+
+
+def test_submit_convert_casts_and_applies_dmatrix_list_rule():
+    """kb_submit_convert: float64 rows into a float32 batch are numpy's astype;
+    KB_IN_XGB_LIST applies xgboost's DMatrix(list) rule as
+    tree_model.xgb_matrix_from_list does (0 -> NaN, NaN -> +inf); float32 rows
+    into a float64 batch are exact; strided views are read in place."""
+    from kfserving_amd.batcher.native import KB_IN_XGB_LIST
+    from kfserving_amd.tree_model import xgb_matrix_from_list
+    rng = np.random.default_rng(9)
+    X = rng.standard_normal((40, 3)) * 10.0 ** rng.integers(-40, 40, (40, 3))
+    X[rng.random(X.shape) < 0.2] = 0.0
+    X[rng.random(X.shape) < 0.1] = np.nan
+    X[0, 0], X[1, 1], X[2, 2] = 1e300, -1e300, np.nextafter(0.0, 1.0)
+
+    async def go():
+        b32, b64 = identity_batcher(TI_F32), identity_batcher(TI_F64)
+        r = {}
+        r["cast"], _ = await b32.submit(X)
+        r["xgb"], _ = await b32.submit(X, KB_IN_XGB_LIST)
+        Xw = np.concatenate([X, X], axis=1)[:, :3]                # row stride 6
+        r["strided"], _ = await b32.submit(Xw)
+        r["f32_to_f64"], _ = await b64.submit(X.astype(np.float32))
+        r["f32_strided_xgb"], _ = await b64.submit(
+            np.concatenate([X, X], axis=1).astype(np.float32)[:, 3:], KB_IN_XGB_LIST)
+        b32.close()
+        b64.close()
+        return r
+    with np.errstate(over="ignore"):
+        r = run(go())
+        want32 = X.astype(np.float32)
+    same = lambda a, b: np.array_equal(a, b, equal_nan=True) and a.dtype == b.dtype
+    assert same(r["cast"], want32) and same(r["strided"], want32)
+    assert same(r["xgb"], xgb_matrix_from_list(X))
+    assert same(r["f32_to_f64"], want32.astype(np.float64))
+    assert same(r["f32_strided_xgb"], xgb_matrix_from_list(want32.astype(np.float64)).astype(np.float64))
