@@ -373,6 +373,11 @@ class NativeModelBatcher:
     def close(self) -> None:
         self._nb.close()
 
+    async def aclose(self) -> None:
+        """Answer every request already submitted, then stop the threads."""
+        await self._nb.drain()
+        self._nb.close()
+
 
 def native_batching_enabled(model) -> bool:
     """The native batcher fronts models that declare it (the GPU tree

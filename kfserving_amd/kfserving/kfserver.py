@@ -290,11 +290,7 @@ class Application:
             # widths can neither fail a batch of well-formed requests nor grow
             # the batcher table.  A model that does not state its width is not
             # batched: requests of different widths could share a batch
-            key = (name, "tensor")
-            batcher = self._batchers.get(key)
-            if batcher is None or batcher.model is not model:
-                batcher = self._batcher_factory(model, self._call, "tensor")
-                self._batchers[key] = batcher
+            batcher = self._batcher_for(model, name, "tensor")
             response = await batcher.submit(X)
             if response.get("predictions") is None:
                 raise HTTPError(500, response.get("message") or "Failed to predict")
@@ -306,6 +302,30 @@ class Application:
                 raise HTTPError(500, "Failed to predict %s" % e)
         hdrs, payload = v2.encode_response(name, req, np.asarray(result))
         return 200, "OK", hdrs, payload
+
+    def _batcher_for(self, model, name: str, kind: str):
+        """One batcher per model and request kind, made on first use; a model
+        object replaced under the same name (a reload) gets a new one."""
+        key = (name, kind)
+        batcher = self._batchers.get(key)
+        if batcher is None or batcher.model is not model:
+            if batcher is not None:
+                self._retire(batcher)
+            batcher = self._batcher_factory(model, self._call, kind)
+            self._batchers[key] = batcher
+        return batcher
+
+    @staticmethod
+    def _retire(batcher) -> None:
+        # a native batcher owns threads and an eventfd: it answers what it
+        # holds, then stops (the asyncio batcher needs nothing)
+        aclose = getattr(batcher, "aclose", None)
+        if aclose is not None:
+            asyncio.ensure_future(aclose())
+
+    def retire_batchers(self, name: str) -> None:
+        for key in [k for k in self._batchers if k[0] == name]:
+            self._retire(self._batchers.pop(key))
 
     async def _predict_request(self, model, name, request):
         """predict -> postprocess, through the batcher when one is configured:
@@ -322,11 +342,7 @@ class Application:
                 except Exception as e:
                     raise HTTPError(500, "Failed to predict %s" % e)
             if kind is not None:
-                key = (name, kind)
-                batcher = self._batchers.get(key)
-                if batcher is None or batcher.model is not model:
-                    batcher = self._batcher_factory(model, self._call, kind)
-                    self._batchers[key] = batcher
+                batcher = self._batcher_for(model, name, kind)
                 response = await batcher.submit(chunk)
                 return model.postprocess(response)
         response = await self._call(model.predict, request)
@@ -375,6 +391,7 @@ class Application:
     async def unload(self, headers, body, name):
         try:
             self.models.unload(name)
+            self.retire_batchers(name)
         except KeyError:
             raise HTTPError(404, "Model with name %s does not exist." % name)
         return _ok(json.dumps({"name": name, "unload": True}))

@@ -309,3 +309,38 @@ def test_submit_convert_casts_and_applies_dmatrix_list_rule():
     assert same(r["xgb"], xgb_matrix_from_list(X))
     assert same(r["f32_to_f64"], want32.astype(np.float64))
     assert same(r["f32_strided_xgb"], xgb_matrix_from_list(want32.astype(np.float64)).astype(np.float64))
+
+
+def test_server_retires_native_batchers(golden, tmp_path):
+    """A reloaded model gets a new native batcher and an unloaded one loses
+    its batchers; a retired batcher answers what it holds, then stops its
+    threads (NativeModelBatcher.aclose)."""
+    import json as _json
+    from kfserving_amd.kfserving import KFServer
+    from kfserving_amd.kfserving.kfmodel_repository import KFModelRepository
+    from tests.test_lgb_batching import _lgb_model, _requests
+    model = _lgb_model(golden, tmp_path)
+    repo = KFModelRepository()
+    repo.update(model)
+    app = KFServer(max_batchsize=64, max_latency_ms=2,
+                   registered_models=repo).create_application()
+    body = _json.dumps(_requests(1)[0]).encode()
+
+    async def go():
+        code, _, _, out = await app.handle("POST", "/v1/models/lightgbm:predict", {}, body)
+        assert code == 200 and _json.loads(out)["batchId"]
+        first = app._batchers[("lightgbm", "inputs")]
+        # a new model object under the same name: a new batcher, the old retired
+        clone = type(model).__new__(type(model))
+        clone.__dict__.update(model.__dict__)
+        repo.update(clone)
+        code, _, _, out = await app.handle("POST", "/v1/models/lightgbm:predict", {}, body)
+        assert code == 200
+        second = app._batchers[("lightgbm", "inputs")]
+        assert second is not first and second.model is clone
+        await asyncio.sleep(0.05)
+        assert first._nb._h is None                      # threads stopped
+        app.retire_batchers("lightgbm")
+        await asyncio.sleep(0.05)
+        assert not app._batchers and second._nb._h is None
+    run(go())
