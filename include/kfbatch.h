@@ -127,6 +127,16 @@ int kb_submit(void* batcher, const void* X, int64_t rows, int64_t row_stride, vo
 int kb_submit_convert(void* batcher, const void* X, int32_t x_dtype, int64_t rows,
                       int64_t row_stride, int32_t transform, void* out, uint64_t tag);
 
+/* Completions of requests whose tag has KB_TAG_CALLBACK set go to `fn`,
+ * called on a model thread (with the batcher's completion lock held: it must
+ * not call back into the batcher), instead of the kb_poll queue; the native
+ * HTTP front end (include/kfhttp.h) answers its connections this way while
+ * the event loop polls the same batcher for its own requests.  NULL fn: every
+ * completion is queued. */
+#define KB_TAG_CALLBACK (1ULL << 63)
+typedef void (*kb_done_fn)(void* ctx, const kb_completion* c);
+int kb_set_done_callback(void* batcher, kb_done_fn fn, void* ctx);
+
 /* Move up to `cap` completions into `out`; returns how many (0: none). */
 int kb_poll(void* batcher, kb_completion* out, int32_t cap);
 

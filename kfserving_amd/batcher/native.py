@@ -34,7 +34,7 @@ KB_OK, KB_ERR_INVALID, KB_ERR_CLOSED, KB_ERR_SYSTEM, KB_ERR_MODEL = 0, -1, -2, -
 KB_IN_PLAIN, KB_IN_XGB_LIST = 0, 1   # kb_submit_convert transforms
 
 EXPORTED_SYMBOLS = ("kb_create", "kb_destroy", "kb_flush", "kb_notify_fd", "kb_submit",
-                    "kb_submit_convert", "kb_poll",
+                    "kb_submit_convert", "kb_set_done_callback", "kb_poll",
                     "kb_batch_message", "kb_get_stats", "kb_now_ns", "kb_loadgen",
                     "kb_abi_version")
 
@@ -93,6 +93,8 @@ def load_library() -> ctypes.CDLL:
     lib.kb_submit.argtypes = [vp, vp, i64, i64, vp, u64]
     lib.kb_submit_convert.restype = ctypes.c_int
     lib.kb_submit_convert.argtypes = [vp, vp, i32, i64, i64, i32, vp, u64]
+    lib.kb_set_done_callback.restype = ctypes.c_int
+    lib.kb_set_done_callback.argtypes = [vp, vp, vp]
     lib.kb_poll.restype = ctypes.c_int
     lib.kb_poll.argtypes = [vp, ctypes.POINTER(KbCompletion), i32]
     lib.kb_batch_message.restype = ctypes.c_int

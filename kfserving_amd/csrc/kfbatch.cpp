@@ -68,6 +68,8 @@ struct Batcher {
   kb_predict_fn predict = nullptr;
   void* model = nullptr;
   kb_error_fn err = nullptr;
+  kb_done_fn done_fn = nullptr;   // completions of KB_TAG_CALLBACK requests
+  void* done_ctx = nullptr;
   size_t x_row = 0, o_row = 0;   // bytes per input / output row
   int64_t max_rows = 0, max_latency_ns = 0;
   int efd = -1;
@@ -182,6 +184,7 @@ void run_batch(Batcher& b, Batch& bt, std::vector<unsigned char>& out) {
     b.st.model_ms_total += (t1 - t0) * 1e-6;
     if (rc != 0) b.st.failed_batches += 1;
   }
+  bool queued = false;
   {
     std::lock_guard<std::mutex> lk(b.cq_mu);
     for (const Waiter& w : bt.waiters) {
@@ -192,10 +195,15 @@ void run_batch(Batcher& b, Batch& bt, std::vector<unsigned char>& out) {
       c.t_done_ns = done;
       c.batch_seq = bt.seq;
       std::memcpy(c.batch_id, id, sizeof id);
-      b.cq.push_back(c);
+      if ((c.tag & KB_TAG_CALLBACK) && b.done_fn) {
+        b.done_fn(b.done_ctx, &c);   // a native caller's request (kb_set_done_callback)
+      } else {
+        b.cq.push_back(c);
+        queued = true;
+      }
     }
   }
-  signal_fd(b.efd);
+  if (queued) signal_fd(b.efd);
 }
 
 void worker_main(Batcher* bp) {
@@ -309,6 +317,15 @@ int kb_flush(void* h) {
   Batcher& b = *static_cast<Batcher*>(h);
   std::lock_guard<std::mutex> lk(b.mu);
   flush_locked(b, false);
+  return KB_OK;
+}
+
+int kb_set_done_callback(void* h, kb_done_fn fn, void* ctx) {
+  if (!h) return KB_ERR_INVALID;
+  Batcher& b = *static_cast<Batcher*>(h);
+  std::lock_guard<std::mutex> lk(b.cq_mu);
+  b.done_fn = fn;
+  b.done_ctx = ctx;
   return KB_OK;
 }
 

@@ -1,0 +1,945 @@
+// The model server's HTTP/1.1 front end (include/kfhttp.h).
+//
+// IO threads each own an epoll set holding the shared listening socket
+// (EPOLLEXCLUSIVE: one thread takes each connection, across the pre-forked
+// worker processes too), their connections (edge-triggered) and an eventfd on
+// which responses for their connections arrive: the native batcher's
+// completions (kb_set_done_callback, on a model thread) and the Python
+// application's answers (kh_respond).  A connection handles one request at a
+// time, in order, as the Python server does (kfserver.py _serve_conn):
+// requests pipelined behind it wait in its read buffer.
+//
+// The parser follows the Python server's (kfserver.py _read_request): the
+// request line split on single spaces into exactly three parts, header lines
+// partitioned at the first ':' with keys lower-cased and both sides stripped
+// (a later duplicate wins), a Content-Length or a chunked body, lines of at
+// most 2^20 bytes (asyncio's reader limit); a malformed request gets the 400
+// page, a body over max_body_bytes the 413 page, and the connection closes.
+#include "kfhttp.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <charconv>
+#include <cctype>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "kfbatch.h"
+#include "kfserve.h"
+
+namespace {
+
+constexpr size_t kMaxLine = 1u << 20;       // asyncio StreamReader limit (start_server)
+constexpr uint64_t kListen = ~0ULL, kWake = ~0ULL - 1;
+constexpr int kThreadShift = 48;            // tag / id: thread index above the connection id
+
+struct RouteCtx;
+
+struct Route {
+  void* batcher = nullptr;
+  RouteCtx* ctx = nullptr;
+  int n_cols = 0, out_width = 0, out_elem = 0, transform = 0;
+};
+
+struct Conn {
+  uint64_t id = 0;
+  int fd = -1;
+  std::string in;
+  size_t in_off = 0;
+  std::string out;
+  size_t out_off = 0;
+  bool busy = false;         // a request is being answered
+  bool peer_gone = false;    // the peer closed while busy: free on the answer
+  bool close_after = false;  // close once `out` is written
+  bool want_out = false;     // EPOLLOUT armed
+  // the fast-path request in flight
+  Route route;
+  std::vector<unsigned char> res;
+  int64_t rows = 0;
+  bool keep = true;
+  // the request handed to Python (kept until kh_respond)
+  std::string method, target, version, headers, body;
+};
+
+struct Done {
+  uint64_t conn = 0;
+  bool from_python = false;
+  kb_completion c{};
+  std::string bytes;   // Python's response; or the model's error text (failed batch)
+  bool close_after = false;
+};
+
+struct Server;
+
+struct IoThread {
+  Server* srv = nullptr;
+  int idx = 0;
+  int ep = -1, wake = -1;
+  std::thread th;
+  std::mutex mu;                 // done
+  std::deque<Done> done;
+  std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;   // this thread only
+  uint64_t next_id = 1;
+};
+
+struct Pending {
+  uint64_t id;
+  Conn* c;
+};
+
+struct RouteCtx {   // the done callback's context: its server and batcher
+  Server* s = nullptr;
+  void* batcher = nullptr;
+  std::atomic<int64_t> inflight{0};   // requests submitted through it, not yet completed
+};
+
+struct Server {
+  kh_config cfg{};
+  std::vector<std::unique_ptr<IoThread>> io;
+  std::mutex rmu;
+  std::unordered_map<std::string, Route> routes;
+  std::mutex fmu;
+  std::deque<Pending> fq;        // requests for Python
+  std::unordered_map<uint64_t, Conn*> handed;   // id -> connection, until kh_respond
+  int ffd = -1;
+  std::atomic<bool> stop{false};
+  std::atomic<int64_t> n_conn{0}, n_native{0}, n_python{0}, n_bad{0};
+  std::deque<RouteCtx> ctxs;          // stable addresses, freed with the server
+  bool started = false;
+};
+
+void signal_fd(int fd) {
+  const uint64_t one = 1;
+  ssize_t r;
+  do {
+    r = write(fd, &one, sizeof one);
+  } while (r < 0 && errno == EINTR);
+}
+
+void drain_fd(int fd) {
+  uint64_t v;
+  while (read(fd, &v, sizeof v) > 0) {
+  }
+}
+
+// ------------------------------------------------------------- formatting
+// Python's float repr ('r' format, kfserver._json_body -> json.dumps): the
+// shortest round-trip digits, fixed notation when the decimal exponent is in
+// [-4, 16), else d[.ddd]e[+-]XX.
+int repr_double(double v, char* buf, int cap) {
+  std::string s;
+  if (std::isnan(v)) {
+    s = "NaN";
+  } else if (std::isinf(v)) {
+    s = v > 0 ? "Infinity" : "-Infinity";
+  } else if (v == 0.0) {
+    s = std::signbit(v) ? "-0.0" : "0.0";
+  } else {
+    char t[40];
+    auto r = std::to_chars(t, t + sizeof t, v, std::chars_format::scientific);
+    std::string sci(t, r.ptr);
+    bool neg = sci[0] == '-';
+    if (neg) sci.erase(0, 1);
+    const size_t e = sci.find('e');
+    std::string digits = sci.substr(0, e);
+    digits.erase(std::remove(digits.begin(), digits.end(), '.'), digits.end());
+    const int exp10 = std::atoi(sci.c_str() + e + 1);
+    const int decpt = exp10 + 1;
+    const int nd = static_cast<int>(digits.size());
+    if (neg) s += '-';
+    if (decpt <= -4 || decpt > 16) {
+      s += digits[0];
+      if (nd > 1) {
+        s += '.';
+        s.append(digits, 1, std::string::npos);
+      }
+      s += 'e';
+      s += exp10 < 0 ? '-' : '+';
+      const int a = std::abs(exp10);
+      if (a < 10) s += '0';
+      s += std::to_string(a);
+    } else if (decpt <= 0) {
+      s += "0.";
+      s.append(static_cast<size_t>(-decpt), '0');
+      s += digits;
+    } else if (decpt >= nd) {
+      s += digits;
+      s.append(static_cast<size_t>(decpt - nd), '0');
+      s += ".0";
+    } else {
+      s.append(digits, 0, static_cast<size_t>(decpt));
+      s += '.';
+      s.append(digits, static_cast<size_t>(decpt), std::string::npos);
+    }
+  }
+  if (static_cast<int>(s.size()) >= cap) return -1;
+  std::memcpy(buf, s.data(), s.size());
+  buf[s.size()] = '\0';
+  return static_cast<int>(s.size());
+}
+
+void append_double(std::string& o, double v) {
+  char b[48];
+  const int n = repr_double(v, b, sizeof b);
+  o.append(b, static_cast<size_t>(n));
+}
+
+// json.dumps(str) with ensure_ascii (the default): \" \\ \n \r \t \b \f, other
+// controls and every non-ASCII code point as \uXXXX (UTF-16 pairs above the
+// BMP); invalid UTF-8 reads as U+FFFD, as bytes.decode(errors="replace")
+void append_json_string(std::string& o, const std::string& s) {
+  o += '"';
+  auto u = [&](unsigned cp) {
+    char b[8];
+    std::snprintf(b, sizeof b, "\\u%04x", cp);
+    o += b;
+  };
+  for (size_t i = 0; i < s.size();) {
+    unsigned char ch = static_cast<unsigned char>(s[i]);
+    if (ch < 0x80) {
+      switch (ch) {
+        case '"': o += "\\\""; break;
+        case '\\': o += "\\\\"; break;
+        case '\n': o += "\\n"; break;
+        case '\r': o += "\\r"; break;
+        case '\t': o += "\\t"; break;
+        case '\b': o += "\\b"; break;
+        case '\f': o += "\\f"; break;
+        default:
+          if (ch < 0x20) u(ch); else o += static_cast<char>(ch);
+      }
+      ++i;
+      continue;
+    }
+    int n = ch >= 0xF0 ? 3 : ch >= 0xE0 ? 2 : ch >= 0xC0 ? 1 : -1;
+    unsigned cp = n == 3 ? ch & 7u : n == 2 ? ch & 15u : ch & 31u;
+    bool ok = n > 0 && i + static_cast<size_t>(n) < s.size() + 0;
+    for (int k = 1; ok && k <= n; ++k) {
+      if (i + static_cast<size_t>(k) >= s.size()) { ok = false; break; }
+      const unsigned char cc = static_cast<unsigned char>(s[i + static_cast<size_t>(k)]);
+      if ((cc & 0xC0) != 0x80) { ok = false; break; }
+      cp = (cp << 6) | (cc & 63u);
+    }
+    if (!ok || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) {
+      u(0xFFFD);
+      ++i;
+      continue;
+    }
+    if (cp >= 0x10000) {
+      cp -= 0x10000;
+      u(0xD800 + (cp >> 10));
+      u(0xDC00 + (cp & 0x3FF));
+    } else {
+      u(cp);
+    }
+    i += static_cast<size_t>(n) + 1;
+  }
+  o += '"';
+}
+
+// kfserver._serialize: status line, the handler's headers, Content-Length,
+// Server, and Connection: close when the connection ends
+void append_response(std::string& o, int code, const char* reason, const char* ctype,
+                     const std::string& body, bool keep) {
+  o += "HTTP/1.1 ";
+  o += std::to_string(code);
+  o += ' ';
+  o += reason;
+  o += "\r\nContent-Type: ";
+  o += ctype;
+  o += "\r\nContent-Length: ";
+  o += std::to_string(body.size());
+  o += "\r\nServer: kfserving-amd\r\n";
+  if (!keep) o += "Connection: close\r\n";
+  o += "\r\n";
+  o += body;
+}
+
+// kfserver.error_response (tornado's error page)
+void append_error(std::string& o, int code, const char* reason) {
+  const std::string page = "<html><title>" + std::to_string(code) + ": " + reason +
+                           "</title><body>" + std::to_string(code) + ": " + reason +
+                           "</body></html>";
+  append_response(o, code, reason, "text/html; charset=UTF-8", page, false);
+}
+
+// ------------------------------------------------------------------- IO
+void close_conn(IoThread& t, Conn* c) {
+  if (c->fd >= 0) {
+    epoll_ctl(t.ep, EPOLL_CTL_DEL, c->fd, nullptr);
+    close(c->fd);
+    c->fd = -1;
+  }
+  if (c->busy) {   // an answer is still coming: free it then
+    c->peer_gone = true;
+    return;
+  }
+  t.conns.erase(c->id);
+}
+
+void arm_out(IoThread& t, Conn* c, bool on) {
+  if (c->want_out == on || c->fd < 0) return;
+  epoll_event ev{};
+  ev.events = EPOLLIN | EPOLLRDHUP | EPOLLET | (on ? EPOLLOUT : 0u);
+  ev.data.u64 = c->id;
+  epoll_ctl(t.ep, EPOLL_CTL_MOD, c->fd, &ev);
+  c->want_out = on;
+}
+
+// write what is pending; false if the connection was closed
+bool flush_out(IoThread& t, Conn* c) {
+  while (c->out_off < c->out.size()) {
+    const ssize_t n = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off,
+                           MSG_NOSIGNAL);
+    if (n > 0) {
+      c->out_off += static_cast<size_t>(n);
+      continue;
+    }
+    if (n < 0 && errno == EINTR) continue;
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      arm_out(t, c, true);
+      return true;
+    }
+    close_conn(t, c);
+    return false;
+  }
+  c->out.clear();
+  c->out_off = 0;
+  arm_out(t, c, false);
+  if (c->close_after) {
+    shutdown(c->fd, SHUT_WR);
+    close_conn(t, c);
+    return false;
+  }
+  return true;
+}
+
+// one line of the read buffer from `pos` (through '\n'): the line without it,
+// or npos-style failure: 0 = incomplete, -1 = too long
+int take_line(const std::string& in, size_t& pos, std::string& line) {
+  const size_t nl = in.find('\n', pos);
+  if (nl == std::string::npos) return in.size() - pos > kMaxLine ? -1 : 0;
+  if (nl + 1 - pos > kMaxLine) return -1;
+  line.assign(in, pos, nl + 1 - pos);
+  pos = nl + 1;
+  return 1;
+}
+
+std::string strip(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && std::isspace(static_cast<unsigned char>(s[a]))) ++a;
+  while (b > a && std::isspace(static_cast<unsigned char>(s[b - 1]))) --b;
+  return s.substr(a, b - a);
+}
+
+std::string lower(std::string s) {
+  for (char& ch : s) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+  return s;
+}
+
+// int(text) as Python parses a Content-Length / chunk size: optional sign,
+// digits (base 10 or 16), surrounding whitespace; false if it would raise
+bool py_int(const std::string& t, int base, int64_t* v) {
+  const std::string s = strip(t);
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i >= s.size()) return false;
+  int64_t x = 0;
+  for (; i < s.size(); ++i) {
+    const char ch = s[i];
+    int d;
+    if (ch >= '0' && ch <= '9') d = ch - '0';
+    else if (base == 16 && ch >= 'a' && ch <= 'f') d = ch - 'a' + 10;
+    else if (base == 16 && ch >= 'A' && ch <= 'F') d = ch - 'A' + 10;
+    else if (ch == '_' && i > 0 && i + 1 < s.size()) continue;
+    else return false;
+    if (x > (INT64_MAX - d) / base) x = INT64_MAX;   // saturate: far beyond any limit
+    else x = x * base + d;
+  }
+  *v = neg ? -x : x;
+  return true;
+}
+
+enum class Parse { kIncomplete, kDone, kBad, kTooLarge };
+
+struct Req {
+  std::string method, target, version, headers;   // headers: "k: v\n" lines
+  std::unordered_map<std::string, std::string> h;
+  std::string body;
+  size_t end = 0;   // bytes of the read buffer it used
+};
+
+Parse parse_request(const std::string& in, size_t start, int64_t max_body, Req* r) {
+  size_t pos = start;
+  std::string line;
+  int k = take_line(in, pos, line);
+  if (k == 0) return Parse::kIncomplete;
+  if (k < 0) return Parse::kBad;
+  {
+    std::string l = line;
+    while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+    size_t a = l.find(' ');
+    if (a == std::string::npos) return Parse::kBad;
+    size_t b = l.find(' ', a + 1);
+    if (b == std::string::npos || l.find(' ', b + 1) != std::string::npos) return Parse::kBad;
+    r->method = l.substr(0, a);
+    r->target = l.substr(a + 1, b - a - 1);
+    r->version = l.substr(b + 1);
+  }
+  r->headers.clear();
+  r->h.clear();
+  for (;;) {
+    k = take_line(in, pos, line);
+    if (k == 0) return Parse::kIncomplete;
+    if (k < 0) return Parse::kBad;
+    if (line == "\r\n" || line == "\n") break;
+    const size_t c = line.find(':');
+    const std::string key = lower(strip(c == std::string::npos ? line : line.substr(0, c)));
+    const std::string val = c == std::string::npos ? std::string() : strip(line.substr(c + 1));
+    r->h[key] = val;
+    r->headers += key;
+    r->headers += ": ";
+    r->headers += val;
+    r->headers += '\n';
+  }
+  auto te = r->h.find("transfer-encoding");
+  r->body.clear();
+  if (te != r->h.end() && lower(te->second) == "chunked") {
+    int64_t total = 0;
+    for (;;) {
+      k = take_line(in, pos, line);
+      if (k == 0) return Parse::kIncomplete;
+      if (k < 0) return Parse::kBad;
+      std::string sz = line.substr(0, line.find(';'));
+      int64_t n = 0;
+      if (strip(sz).empty()) n = 0;
+      else if (!py_int(sz, 16, &n) || n < 0) return Parse::kBad;
+      if (n == 0) {
+        k = take_line(in, pos, line);   // the line after the last chunk
+        if (k == 0) return Parse::kIncomplete;
+        if (k < 0) return Parse::kBad;
+        break;
+      }
+      total += n;
+      if (total > max_body) return Parse::kTooLarge;
+      if (in.size() - pos < static_cast<size_t>(n)) return Parse::kIncomplete;
+      r->body.append(in, pos, static_cast<size_t>(n));
+      pos += static_cast<size_t>(n);
+      k = take_line(in, pos, line);
+      if (k == 0) return Parse::kIncomplete;
+      if (k < 0) return Parse::kBad;
+    }
+  } else {
+    int64_t n = 0;
+    auto cl = r->h.find("content-length");
+    if (cl != r->h.end() && !cl->second.empty() && !py_int(cl->second, 10, &n)) return Parse::kBad;
+    if (n > max_body) return Parse::kTooLarge;
+    if (n < 0) return Parse::kBad;
+    if (in.size() - pos < static_cast<size_t>(n)) return Parse::kIncomplete;
+    r->body.assign(in, pos, static_cast<size_t>(n));
+    pos += static_cast<size_t>(n);
+  }
+  r->end = pos;
+  return Parse::kDone;
+}
+
+// "/v1/models/<name>:predict" (query string dropped): the model name, or ""
+std::string predict_route(const std::string& target) {
+  const std::string path = target.substr(0, target.find('?'));
+  static const std::string pre = "/v1/models/", suf = ":predict";
+  if (path.size() <= pre.size() + suf.size() || path.compare(0, pre.size(), pre) != 0 ||
+      path.compare(path.size() - suf.size(), suf.size(), suf) != 0)
+    return std::string();
+  std::string name = path.substr(pre.size(), path.size() - pre.size() - suf.size());
+  for (char ch : name)
+    if (!(std::isalnum(static_cast<unsigned char>(ch)) || ch == '_' || ch == '-')) return std::string();
+  return name;
+}
+
+void process(IoThread& t, Conn* c);
+
+void hand_to_python(IoThread& t, Conn* c, Req& r, bool keep) {
+  Server& s = *t.srv;
+  c->method = std::move(r.method);
+  c->target = std::move(r.target);
+  c->version = std::move(r.version);
+  c->headers = std::move(r.headers);
+  c->body = std::move(r.body);
+  c->keep = keep;
+  c->busy = true;
+  const uint64_t id = (static_cast<uint64_t>(t.idx) << kThreadShift) | c->id;
+  {
+    std::lock_guard<std::mutex> lk(s.fmu);
+    s.fq.push_back({id, c});
+    s.handed[id] = c;
+  }
+  s.n_python.fetch_add(1);
+  signal_fd(s.ffd);
+}
+
+// the fast path: true if the request went to the batcher
+bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
+  Server& s = *t.srv;
+  if (r.method != "POST" || r.body.size() >= KF_MT_MIN_BYTES) return false;   // big bodies: the
+  const std::string name = predict_route(r.target);                          // threaded parser
+  if (name.empty()) return false;
+  for (const char* h : {"ce-specversion", "ce-source", "ce-type", "ce-id"})
+    if (r.h.count(h)) return false;   // binary CloudEvents: the application's path
+  Route route;
+  {
+    std::lock_guard<std::mutex> lk(s.rmu);
+    auto it = s.routes.find(name);
+    if (it == s.routes.end()) return false;
+    route = it->second;
+  }
+  thread_local std::vector<double> xb;
+  const size_t cap = (r.body.size() + 1) / 2;
+  if (xb.size() < cap) xb.resize(cap);
+  int64_t rows = 0, cols = 0;
+  if (kf_parse_instances(r.body.data(), static_cast<int64_t>(r.body.size()), xb.data(),
+                         static_cast<int64_t>(xb.size()), &rows, &cols) != KF_PARSED ||
+      rows <= 0 || cols != route.n_cols)
+    return false;
+  c->route = route;
+  c->rows = rows;
+  c->keep = keep;
+  c->res.assign(static_cast<size_t>(rows) * route.out_width * route.out_elem, 0);
+  c->busy = true;
+  const uint64_t tag = KB_TAG_CALLBACK | (static_cast<uint64_t>(t.idx) << kThreadShift) | c->id;
+  route.ctx->inflight.fetch_add(1);
+  if (kb_submit_convert(route.batcher, xb.data(), 1, rows, cols, route.transform, c->res.data(),
+                        tag) != KB_OK) {
+    route.ctx->inflight.fetch_sub(1);
+    c->busy = false;   // the batcher was retired meanwhile: the application answers
+    return false;
+  }
+  s.n_native.fetch_add(1);
+  return true;
+}
+
+// the Python server's bytes for a batched :predict (NativeModelBatcher.submit
+// -> model.postprocess -> _ok -> _json_body)
+void answer_native(Conn* c, const kb_completion& d, const std::string& err) {
+  std::string body;
+  body.reserve(64 + static_cast<size_t>(c->rows) * c->route.out_width * 22);
+  if (d.status == KB_OK) {
+    body += "{\"message\": \"\", \"batchId\": \"";
+    body += d.batch_id;
+    body += "\", \"predictions\": [";
+    const int w = c->route.out_width;
+    for (int64_t i = 0; i < c->rows; ++i) {
+      if (i) body += ", ";
+      if (w > 1) body += '[';
+      for (int j = 0; j < w; ++j) {
+        if (j) body += ", ";
+        const size_t at = static_cast<size_t>(i * w + j);
+        double v;
+        if (c->route.out_elem == 4) {
+          float f;
+          std::memcpy(&f, c->res.data() + at * 4, 4);
+          v = f;
+        } else {
+          std::memcpy(&v, c->res.data() + at * 8, 8);
+        }
+        append_double(body, v);
+      }
+      if (w > 1) body += ']';
+    }
+    body += "]}";
+  } else {
+    body += "{\"message\": ";
+    append_json_string(body, "Failed to predict " + err);
+    body += ", \"batchId\": \"\", \"predictions\": null}";
+    size_t p = 0;   // tornado's json_encode: "</" -> "<\/"
+    while ((p = body.find("</", p)) != std::string::npos) {
+      body.replace(p, 2, "<\\/");
+      p += 3;
+    }
+  }
+  append_response(c->out, 200, "OK", "application/json; charset=UTF-8", body, c->keep);
+  c->close_after = c->close_after || !c->keep;
+  std::vector<unsigned char>().swap(c->res);
+}
+
+void process(IoThread& t, Conn* c) {
+  Server& s = *t.srv;
+  while (!c->busy && c->fd >= 0 && !c->close_after) {
+    if (c->in_off >= c->in.size()) {
+      c->in.clear();
+      c->in_off = 0;
+      return;
+    }
+    Req r;
+    const Parse p = parse_request(c->in, c->in_off, s.cfg.max_body_bytes, &r);
+    if (p == Parse::kIncomplete) {
+      if (c->in_off > (1u << 16)) {   // keep the buffer from growing at its front
+        c->in.erase(0, c->in_off);
+        c->in_off = 0;
+      }
+      return;
+    }
+    if (p == Parse::kBad || p == Parse::kTooLarge) {
+      if (p == Parse::kBad) append_error(c->out, 400, "Bad Request");
+      else append_error(c->out, 413, "Request Entity Too Large");
+      s.n_bad.fetch_add(1);
+      c->close_after = true;
+      c->in.clear();
+      c->in_off = 0;
+      flush_out(t, c);
+      return;
+    }
+    c->in_off = r.end;
+    auto ch = r.h.find("connection");
+    const bool keep = (ch == r.h.end() || lower(ch->second) != "close") && r.version == "HTTP/1.1";
+    if (!try_native(t, c, r, keep)) hand_to_python(t, c, r, keep);
+  }
+}
+
+void on_done(IoThread& t, Done& d) {
+  auto it = t.conns.find(d.conn);
+  if (it == t.conns.end()) return;
+  Conn* c = it->second.get();
+  if (!c->busy) return;
+  if (d.from_python) {
+    c->out += d.bytes;
+    c->close_after = c->close_after || d.close_after;
+    c->method.clear();
+    c->target.clear();
+    c->headers.clear();
+    std::string().swap(c->body);
+  } else {
+    answer_native(c, d.c, d.bytes);
+  }
+  c->busy = false;
+  if (c->peer_gone) {
+    t.conns.erase(it);
+    return;
+  }
+  if (flush_out(t, c)) process(t, c);
+}
+
+void on_readable(IoThread& t, Conn* c) {
+  char buf[65536];
+  for (;;) {
+    const ssize_t n = read(c->fd, buf, sizeof buf);
+    if (n > 0) {
+      c->in.append(buf, static_cast<size_t>(n));
+      continue;
+    }
+    if (n < 0 && errno == EINTR) continue;
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    // EOF or error: what was complete is still answered (the Python
+    // server reads requests until the stream ends), then the connection closes
+    if (!c->busy) process(t, c);
+    if (c->fd >= 0) {
+      if (c->busy) {
+        c->close_after = true;   // answer the request in flight, then close
+      } else if (c->out_off >= c->out.size()) {
+        close_conn(t, c);
+      } else {
+        c->close_after = true;
+      }
+    }
+    return;
+  }
+  process(t, c);
+}
+
+void accept_all(IoThread& t) {
+  Server& s = *t.srv;
+  for (;;) {
+    const int fd = accept4(s.cfg.listen_fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+    if (fd < 0) {
+      if (errno == EINTR) continue;
+      return;   // EAGAIN: another thread or process took it
+    }
+    const int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    auto c = std::make_unique<Conn>();
+    c->id = t.next_id++;
+    c->fd = fd;
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLRDHUP | EPOLLET;
+    ev.data.u64 = c->id;
+    if (epoll_ctl(t.ep, EPOLL_CTL_ADD, fd, &ev) != 0) {
+      close(fd);
+      continue;
+    }
+    Conn* cp = c.get();
+    t.conns.emplace(c->id, std::move(c));
+    s.n_conn.fetch_add(1);
+    on_readable(t, cp);
+  }
+}
+
+void io_main(IoThread* tp) {
+  IoThread& t = *tp;
+  Server& s = *t.srv;
+  epoll_event evs[256];
+  std::deque<Done> local;
+  while (!s.stop.load()) {
+    const int n = epoll_wait(t.ep, evs, 256, 200);
+    for (int i = 0; i < n; ++i) {
+      const uint64_t key = evs[i].data.u64;
+      if (key == kListen) {
+        accept_all(t);
+      } else if (key == kWake) {
+        drain_fd(t.wake);
+        {
+          std::lock_guard<std::mutex> lk(t.mu);
+          local.swap(t.done);
+        }
+        for (Done& d : local) on_done(t, d);
+        local.clear();
+      } else {
+        auto it = t.conns.find(key);
+        if (it == t.conns.end()) continue;
+        Conn* c = it->second.get();
+        if (evs[i].events & EPOLLOUT) {
+          if (!flush_out(t, c)) continue;
+          if (!c->busy) process(t, c);
+          if (t.conns.find(key) == t.conns.end() || c->fd < 0) continue;
+        }
+        if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) on_readable(t, c);
+      }
+    }
+  }
+}
+
+void native_done(void* ctx, const kb_completion* c) {
+  RouteCtx& rc = *static_cast<RouteCtx*>(ctx);
+  Server& s = *rc.s;
+  const size_t ti = static_cast<size_t>((c->tag & ~KB_TAG_CALLBACK) >> kThreadShift);
+  if (ti >= s.io.size()) return;
+  IoThread& t = *s.io[ti];
+  Done d;
+  d.conn = c->tag & ((1ULL << kThreadShift) - 1);
+  d.c = *c;
+  if (c->status != KB_OK) {   // the text now, while the batcher surely exists
+    char m[4096];
+    // kb_batch_message takes the message lock, not the completion lock held here
+    const int n = kb_batch_message(rc.batcher, c->batch_seq, m, sizeof m);
+    d.bytes = n >= 0 ? std::string(m, static_cast<size_t>(n)) : std::string("model call failed");
+  }
+  {
+    std::lock_guard<std::mutex> lk(t.mu);
+    t.done.push_back(std::move(d));
+  }
+  rc.inflight.fetch_sub(1);
+  signal_fd(t.wake);
+}
+
+// no new requests reach the route's batcher (removed from the table): send
+// what it holds to the model, wait for those requests' completions, then
+// detach the callback, after which the application may destroy the batcher
+void detach(RouteCtx* ctx) {
+  kb_flush(ctx->batcher);
+  for (int i = 0; i < 400000 && ctx->inflight.load() > 0; ++i) usleep(50);
+  kb_set_done_callback(ctx->batcher, nullptr, nullptr);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t kh_abi_version(void) { return KH_ABI_VERSION; }
+
+int kh_repr_double(double v, char* buf, int32_t cap) {
+  if (!buf || cap <= 0) return -1;
+  return repr_double(v, buf, cap);
+}
+
+int kh_create(const kh_config* cfg, void** out) {
+  if (!cfg || !out || cfg->abi_version != KH_ABI_VERSION || cfg->listen_fd < 0 ||
+      cfg->io_threads < 1 || cfg->io_threads > 256)
+    return -1;
+  *out = nullptr;
+  auto s = std::make_unique<Server>();
+  s->cfg = *cfg;
+  if (s->cfg.max_body_bytes <= 0) s->cfg.max_body_bytes = 104857600;
+  s->ffd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  if (s->ffd < 0) return -3;
+  for (int i = 0; i < cfg->io_threads; ++i) {
+    auto t = std::make_unique<IoThread>();
+    t->srv = s.get();
+    t->idx = i;
+    t->ep = epoll_create1(EPOLL_CLOEXEC);
+    t->wake = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (t->ep < 0 || t->wake < 0) return -3;
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLEXCLUSIVE;
+    ev.data.u64 = kListen;
+    if (epoll_ctl(t->ep, EPOLL_CTL_ADD, cfg->listen_fd, &ev) != 0) return -3;
+    epoll_event wv{};
+    wv.events = EPOLLIN;
+    wv.data.u64 = kWake;
+    if (epoll_ctl(t->ep, EPOLL_CTL_ADD, t->wake, &wv) != 0) return -3;
+    s->io.push_back(std::move(t));
+  }
+  *out = s.release();
+  return 0;
+}
+
+int kh_add_v1_predict(void* h, const char* model, void* batcher, int32_t n_cols,
+                      int32_t out_width, int32_t out_elem_bytes, int32_t transform) {
+  if (!h || !model || !batcher || n_cols <= 0 || out_width <= 0 ||
+      (out_elem_bytes != 4 && out_elem_bytes != 8))
+    return -1;
+  Server& s = *static_cast<Server*>(h);
+  RouteCtx* ctx;
+  {
+    std::lock_guard<std::mutex> lk(s.rmu);
+    if (s.routes.count(model)) return -1;   // remove the old route first (kh_remove_route)
+    s.ctxs.emplace_back();
+    ctx = &s.ctxs.back();
+    ctx->s = &s;
+    ctx->batcher = batcher;
+  }
+  if (kb_set_done_callback(batcher, native_done, ctx) != KB_OK) return -1;
+  Route r;
+  r.batcher = batcher;
+  r.ctx = ctx;
+  r.n_cols = n_cols;
+  r.out_width = out_width;
+  r.out_elem = out_elem_bytes;
+  r.transform = transform;
+  std::lock_guard<std::mutex> lk(s.rmu);
+  s.routes[model] = r;
+  return 0;
+}
+
+int kh_remove_route(void* h, const char* model) {
+  if (!h || !model) return -1;
+  Server& s = *static_cast<Server*>(h);
+  RouteCtx* ctx;
+  {
+    std::lock_guard<std::mutex> lk(s.rmu);
+    auto it = s.routes.find(model);
+    if (it == s.routes.end()) return -1;
+    ctx = it->second.ctx;
+    s.routes.erase(it);
+  }
+  detach(ctx);
+  return 0;
+}
+
+int kh_start(void* h) {
+  if (!h) return -1;
+  Server& s = *static_cast<Server*>(h);
+  if (s.started) return -1;
+  s.started = true;
+  for (auto& t : s.io) t->th = std::thread(io_main, t.get());
+  return 0;
+}
+
+int kh_fallback_fd(void* h) { return h ? static_cast<Server*>(h)->ffd : -1; }
+
+int kh_next_fallback(void* h, kh_request* req) {
+  if (!h || !req) return -1;
+  Server& s = *static_cast<Server*>(h);
+  std::lock_guard<std::mutex> lk(s.fmu);
+  if (s.fq.empty()) return 0;
+  const Pending p = s.fq.front();
+  s.fq.pop_front();
+  Conn* c = p.c;
+  req->id = p.id;
+  req->method = c->method.c_str();
+  req->target = c->target.c_str();
+  req->version = c->version.c_str();
+  req->headers = c->headers.data();
+  req->headers_len = static_cast<int64_t>(c->headers.size());
+  req->body = c->body.data();
+  req->body_len = static_cast<int64_t>(c->body.size());
+  req->keep_alive = c->keep ? 1 : 0;
+  req->reserved = 0;
+  return 1;
+}
+
+int kh_respond(void* h, uint64_t id, const void* data, int64_t len, int32_t close_after) {
+  if (!h || (!data && len > 0) || len < 0) return -1;
+  Server& s = *static_cast<Server*>(h);
+  {
+    std::lock_guard<std::mutex> lk(s.fmu);
+    if (!s.handed.erase(id)) return -1;
+  }
+  const size_t ti = static_cast<size_t>(id >> kThreadShift);
+  if (ti >= s.io.size()) return -1;
+  IoThread& t = *s.io[ti];
+  Done d;
+  d.conn = id & ((1ULL << kThreadShift) - 1);
+  d.from_python = true;
+  d.bytes.assign(static_cast<const char*>(data), static_cast<size_t>(len));
+  d.close_after = close_after != 0;
+  {
+    std::lock_guard<std::mutex> lk(t.mu);
+    t.done.push_back(std::move(d));
+  }
+  signal_fd(t.wake);
+  return 0;
+}
+
+int kh_get_stats(void* h, kh_stats* st) {
+  if (!h || !st) return -1;
+  Server& s = *static_cast<Server*>(h);
+  st->connections = s.n_conn.load();
+  st->native_requests = s.n_native.load();
+  st->python_requests = s.n_python.load();
+  st->bad_requests = s.n_bad.load();
+  return 0;
+}
+
+int kh_destroy(void* h) {
+  if (!h) return -1;
+  Server* s = static_cast<Server*>(h);
+  s->stop.store(true);
+  for (auto& t : s->io) signal_fd(t->wake);
+  for (auto& t : s->io)
+    if (t->th.joinable()) t->th.join();
+  // requests still on a batcher write into their connection's buffer: every
+  // route is detached (its completions arrive in the stopped threads' queues)
+  // before anything is freed
+  std::vector<RouteCtx*> live;
+  {
+    std::lock_guard<std::mutex> lk(s->rmu);
+    for (auto& kv : s->routes) live.push_back(kv.second.ctx);
+    s->routes.clear();
+  }
+  for (RouteCtx* c : live) detach(c);
+  for (auto& t : s->io) {
+    for (auto& kv : t->conns)
+      if (kv.second->fd >= 0) close(kv.second->fd);
+    t->conns.clear();
+    epoll_ctl(t->ep, EPOLL_CTL_DEL, s->cfg.listen_fd, nullptr);
+    close(t->ep);
+    close(t->wake);
+  }
+  close(s->ffd);
+  delete s;
+  return 0;
+}
+
+}  // extern "C"

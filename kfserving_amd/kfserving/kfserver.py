@@ -59,6 +59,8 @@ parser.add_argument('--max_batchsize', default=0, type=int,
                     help='Enable the in-process batcher with this many rows per batch (0 = off).')
 parser.add_argument('--max_latency_ms', default=5000, type=int,
                     help='Batcher flush latency in milliseconds.')
+parser.add_argument('--http_io_threads', default=2, type=int,
+                    help='IO threads of the native HTTP front end per worker process.')
 parser.add_argument('--no_fast_json', action='store_true',
                     help='Decode every body with json.loads (no native v1 parser).')
 args, _ = parser.parse_known_args()
@@ -157,6 +159,7 @@ class Application:
         self.executor = executor or ThreadPoolExecutor(max_workers=8)
         self._batchers = {}
         self._batcher_factory = batcher_factory
+        self.batcher_listeners = []
         name = r"([a-zA-Z0-9_-]+)"
         self.routes = [
             (re.compile(r"^/$"), self.liveness),
@@ -305,18 +308,23 @@ class Application:
 
     def _batcher_for(self, model, name: str, kind: str):
         """One batcher per model and request kind, made on first use; a model
-        object replaced under the same name (a reload) gets a new one."""
+        object replaced under the same name (a reload) gets a new one.
+        Listeners (the native HTTP front end) hear of every batcher made and
+        retired: ``listener(event, name, kind, batcher)``."""
         key = (name, kind)
         batcher = self._batchers.get(key)
         if batcher is None or batcher.model is not model:
             if batcher is not None:
-                self._retire(batcher)
+                self._retire(key, batcher)
             batcher = self._batcher_factory(model, self._call, kind)
             self._batchers[key] = batcher
+            for fn in self.batcher_listeners:
+                fn("create", name, kind, batcher)
         return batcher
 
-    @staticmethod
-    def _retire(batcher) -> None:
+    def _retire(self, key, batcher) -> None:
+        for fn in self.batcher_listeners:   # before it stops: nothing may submit to it
+            fn("retire", key[0], key[1], batcher)
         # a native batcher owns threads and an eventfd: it answers what it
         # holds, then stops (the asyncio batcher needs nothing)
         aclose = getattr(batcher, "aclose", None)
@@ -325,7 +333,7 @@ class Application:
 
     def retire_batchers(self, name: str) -> None:
         for key in [k for k in self._batchers if k[0] == name]:
-            self._retire(self._batchers.pop(key))
+            self._retire(key, self._batchers.pop(key))
 
     async def _predict_request(self, model, name, request):
         """predict -> postprocess, through the batcher when one is configured:
@@ -384,6 +392,9 @@ class Application:
             ex_type, ex_value, _ = sys.exc_info()
             raise HTTPError(500, f"Model with name {name} is not ready. "
                                  f"Error type: {ex_type} error msg: {ex_value}")
+        # the repository may hold a new model object now: its batchers (and
+        # the native front end's route on them) are made afresh on the next request
+        self.retire_batchers(name)
         if not self.models.is_model_ready(name):
             raise HTTPError(503, f"Model with name {name} is not ready.")
         return _ok(json.dumps({"name": name, "load": True}))
@@ -460,7 +471,8 @@ class KFServer:
                  registered_models: KFModelRepository = None,
                  max_batchsize: int = args.max_batchsize,
                  max_latency_ms: int = args.max_latency_ms,
-                 fast_json: bool = not args.no_fast_json):
+                 fast_json: bool = not args.no_fast_json,
+                 http_io_threads: int = args.http_io_threads):
         self.registered_models = registered_models if registered_models is not None \
             else KFModelRepository()
         self.http_port = http_port
@@ -470,6 +482,9 @@ class KFServer:
         self.max_batchsize = max_batchsize
         self.max_latency_ms = max_latency_ms
         self.fast_json = fast_json
+        self.http_io_threads = max(1, int(http_io_threads))
+        self.front_end = None
+        self.native_http: Optional[bool] = None   # None: KF_NATIVE_HTTP (default on)
         self._server = None
         self._sock: Optional[socket.socket] = None
 
@@ -538,9 +553,27 @@ class KFServer:
         return sock
 
     async def serve(self, sock: Optional[socket.socket] = None) -> None:
-        """Serve on an already-bound socket until cancelled (used by tests)."""
+        """Serve on an already-bound socket until cancelled (used by tests).
+
+        With batching on and a model the native HTTP front end can answer
+        (kfserving.native_http: xgbserver models), the socket is served by
+        native IO threads -- batched v1 :predict requests never enter the
+        interpreter, every other request is handed to the same Application --
+        unless KF_NATIVE_HTTP=0."""
         app = self.create_application()
         sock = sock or self._sock or self.bind()
+        from . import native_http
+        use = self.native_http if self.native_http is not None else native_http.native_http_enabled()
+        if use and any(
+                native_http.route_spec_static(app, m) for m in app.models.get_models()):
+            fe = native_http.NativeFrontEnd(app, sock, io_threads=self.http_io_threads,
+                                            max_body=self.max_buffer_size)
+            fe.add_routes()
+            if fe.routes:
+                self.front_end = fe
+                await fe.serve_forever()
+                return
+            fe.close()
         self._server = await asyncio.start_server(
             lambda r, w: self._serve_conn(app, r, w), sock=sock, limit=2 ** 20)
         async with self._server:

@@ -51,6 +51,10 @@ class XGBoostModel(GPUForestMixin, KFModel):
             X = X.reshape(1, -1)
         return X if X.dtype == np.float32 else X.astype(np.float32)
 
+    # the native HTTP front end answers batched v1 :predict bodies of this
+    # model itself, with DMatrix(list)'s element rule (kfbatch.h KB_IN_XGB_LIST)
+    native_v1_transform = 1
+
     def native_request(self, chunk, kind: str):
         # a natively decoded JSON list: DMatrix(list)'s rule (0 missing, NaN
         # right) and the float32 cast are applied by the native batcher while

@@ -107,6 +107,9 @@ def main():
     p.add_argument("--model", default="c2", choices=["c2", "dummy"])
     p.add_argument("--max-batch", type=int, default=65536)
     p.add_argument("--max-latency-ms", type=int, default=5)
+    p.add_argument("--io-threads", type=int, default=2,
+                   help="native HTTP front end IO threads per worker (KF_NATIVE_HTTP=0: "
+                        "the asyncio server)")
     args = p.parse_args()
     soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
     resource.setrlimit(resource.RLIMIT_NOFILE, (hard, hard))
@@ -120,7 +123,8 @@ def main():
         cmd = [sys.executable, "-m", "kfserving_amd.xgbserver", "--model_dir", tmp,
                "--model_name", "model", "--http_port", str(args.port),
                "--workers", str(args.workers), "--max_batchsize", str(args.max_batch),
-               "--max_latency_ms", str(args.max_latency_ms)]
+               "--max_latency_ms", str(args.max_latency_ms),
+               "--http_io_threads", str(args.io_threads)]
     else:
         code = DUMMY_SERVER % {"root": ROOT, "port": args.port, "workers": args.workers,
                                "mbs": args.max_batch, "lat": args.max_latency_ms}
@@ -145,6 +149,9 @@ def main():
                                   "in-process batcher", "model": args.model,
                         "workers": args.workers, "max_batch_size": args.max_batch,
                         "max_latency_ms": args.max_latency_ms,
+                        "native_http": os.environ.get("KF_NATIVE_HTTP", "1") != "0",
+                        "native_batcher": os.environ.get("KF_NATIVE_BATCHER", "1") != "0",
+                        "io_threads": args.io_threads,
                         "gpus_visible": os.environ.get("TREEINFER_DEVICES", "all")})
             print(json.dumps(res), flush=True)
     finally:

@@ -1,0 +1,266 @@
+"""The native HTTP front end (include/kfhttp.h, libkfserve.so), CPU only:
+every response must be the Python server's bytes for the same request
+(python/kfserving/test/test_server.py's byte contracts are the reference's).
+The xgbserver model's device call is replaced by the canonical numpy
+evaluator, so the native route's batches go through the native batcher to a
+Python model behind the same function pointer; the -m gpu twin is
+tests/test_gpu_native_http.py."""
+import http.client
+import json
+import os
+import re
+import shutil
+import socket
+import struct
+import time
+
+import numpy as np
+import pytest
+
+from kfserving_amd.forest import OUT_PREDICT
+from kfserving_amd.kfserving import KFServer
+from kfserving_amd.kfserving.native_http import EXPORTED_SYMBOLS, load_library, repr_double
+from tests import canon_eval
+from tests.test_server import _Running
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_header_declares_the_binding_symbols():
+    import subprocess
+    src = open(os.path.join(ROOT, "include", "kfhttp.h")).read()
+    names = sorted(set(re.findall(r"^\s*(?:int|int32_t)\s+(kh_\w+)\(", src, re.M)))
+    assert names == sorted(EXPORTED_SYMBOLS)
+    lib = load_library()
+    out = subprocess.run(["nm", "-D", "--defined-only", lib._name], capture_output=True,
+                         text=True, check=True).stdout
+    assert set(names) <= set(re.findall(r"\bT (kh_\w+)", out))
+
+
+def test_repr_double_matches_python():
+    rng = np.random.default_rng(1)
+    vals = [0.0, -0.0, 1.0, -1.0, 0.5, 0.1, 1e16, 1e15, 9999999999999998.0, 1e-4, 1e-5,
+            0.0001234, 123456789012345678.0, 5e-324, 1.7976931348623157e308, 2.5e-7,
+            float("nan"), float("inf"), float("-inf"), 100.0, 1e22, 1e21, 0.001, 12.5]
+    vals += list(rng.standard_normal(2000) * 10.0 ** rng.integers(-30, 30, 2000))
+    vals += [float(np.float32(v)) for v in rng.standard_normal(2000)]
+    vals += [float(v) for v in rng.uniform(0, 1, 500).astype(np.float32)]
+    for v in vals:
+        assert repr_double(v) == json.dumps(v), v
+
+
+def _xgb_model(golden, tmp_path, name="xgboost-iris"):
+    from kfserving_amd.xgbserver import XGBoostModel
+    d = tmp_path / name
+    d.mkdir(parents=True)
+    shutil.copy(os.path.join(golden, "xgb_iris_legacy_082.bst"), str(d / "model.bst"))
+    m = XGBoostModel(name, str(d), 1)
+    m.load()
+    m.predict_matrix = lambda X, kind=OUT_PREDICT: canon_eval.predict(m._forest, X, kind)
+    return m
+
+
+def _servers(golden, tmp_path, **kw):
+    """The same model behind the native front end and behind the Python server."""
+    out = []
+    for native in (True, False):
+        srv = KFServer(max_batchsize=kw.get("batch", 64), max_latency_ms=kw.get("lat", 3))
+        srv.native_http = native
+        srv.register_model(_xgb_model(golden, tmp_path / ("n" if native else "p")))
+        out.append(_Running(srv))
+    time.sleep(0.2)
+    return out
+
+
+def _raw(port, data: bytes, timeout=10.0) -> bytes:
+    s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
+    s.sendall(data)
+    chunks = []
+    try:
+        while True:
+            b = s.recv(65536)
+            if not b:
+                break
+            chunks.append(b)
+    except socket.timeout:
+        pass
+    s.close()
+    return b"".join(chunks)
+
+
+def _norm(b: bytes) -> bytes:
+    return re.sub(rb'"batchId": "[0-9a-f-]{36}"', b'"batchId": "ID"', b)
+
+
+def _iris_bodies():
+    from sklearn.datasets import load_iris
+    X = load_iris()["data"]
+    rng = np.random.default_rng(0)
+    bodies = []
+    for i in range(12):
+        rows = X[rng.integers(0, 150, int(rng.integers(1, 9)))].tolist()
+        if i % 4 == 1:
+            rows[0][1] = 0            # DMatrix(list): 0 is missing
+        bodies.append(json.dumps({"instances": rows}).encode())
+    bodies.append(b'{"instances": [[6.8, 2.8, 4.8, 1.4], [6.0, 3.4, 4.5, 1.6]]}')
+    bodies.append(b'{ "instances" : [ [ NaN, 1e-3, -0.0, Infinity ] ] }')
+    return bodies
+
+
+def test_native_predict_bytes_equal_python_server(golden, tmp_path):
+    nat, py = _servers(golden, tmp_path)
+    try:
+        fe = nat.server.front_end
+        assert fe is not None and "xgboost-iris" in fe.routes
+        for body in _iris_bodies():
+            a = nat.fetch("/v1/models/xgboost-iris:predict", "POST", body)
+            b = py.fetch("/v1/models/xgboost-iris:predict", "POST", body)
+            assert a[0] == b[0] == 200
+            assert {k: v for k, v in a[1].items()} == {k: v for k, v in b[1].items()}
+            assert _norm(a[2]) == _norm(b[2])
+            assert json.loads(a[2])["batchId"]
+        st = fe.stats()
+        assert st["native_requests"] >= 14 and st["python_requests"] == 0
+    finally:
+        nat.stop()
+        py.stop()
+
+
+def test_fallback_routes_and_errors_equal_python_server(golden, tmp_path):
+    nat, py = _servers(golden, tmp_path)
+    cases = [
+        ("/", "GET", None, {}),
+        ("/v1/models", "GET", None, {}),
+        ("/v1/models/xgboost-iris", "GET", None, {}),
+        ("/v1/models/nope", "GET", None, {}),
+        ("/v1/models/nope:predict", "POST", b'{"instances": [[1, 2, 3, 4]]}', {}),
+        ("/v1/models/xgboost-iris:predict", "POST", b'{"instances": 3}', {}),
+        ("/v1/models/xgboost-iris:predict", "POST", b'not json', {}),
+        ("/v1/models/xgboost-iris:predict", "POST", b'{"instances": [[1, 2, 3]]}', {}),
+        ("/v1/models/xgboost-iris:predict", "GET", None, {}),
+        ("/v1/models/xgboost-iris:predict?x=1", "POST", b'{"instances": [[1, 2, 3, 4]]}', {}),
+        ("/v2/models/xgboost-iris/infer", "POST",
+         json.dumps({"inputs": [{"name": "x", "shape": [1, 4], "datatype": "FP32",
+                                 "data": [1, 2, 3, 4]}]}).encode(), {}),
+        ("/v1/models/xgboost-iris:predict", "POST", b'{"instances": [[1, 2, 3, 4]]}',
+         {"ce-specversion": "1.0", "ce-source": "s", "ce-type": "t", "ce-id": "1",
+          "content-type": "application/json"}),
+    ]
+    try:
+        for path, method, body, hdrs in cases:
+            a = nat.fetch(path, method, body, hdrs)
+            b = py.fetch(path, method, body, hdrs)
+            a_h = {k: v for k, v in a[1].items() if k.lower() not in ("ce-time", "ce-id")}
+            b_h = {k: v for k, v in b[1].items() if k.lower() not in ("ce-time", "ce-id")}
+            assert (a[0], a_h) == (b[0], b_h), (path, method)
+            assert _norm(a[2]) == _norm(b[2]), (path, method, a[2], b[2])
+        assert nat.server.front_end.stats()["python_requests"] >= len(cases) - 1
+    finally:
+        nat.stop()
+        py.stop()
+
+
+def test_malformed_requests_and_framing(golden, tmp_path):
+    """400 / 413 pages and closes, chunked bodies, keep-alive, pipelining and
+    Connection: close, byte for byte as the Python server."""
+    nat, py = _servers(golden, tmp_path)
+    body = b'{"instances": [[6.8, 2.8, 4.8, 1.4]]}'
+    req = (b"POST /v1/models/xgboost-iris:predict HTTP/1.1\r\nHost: x\r\n"
+           b"Content-Length: %d\r\n\r\n" % len(body)) + body
+    chunked = (b"POST /v1/models/xgboost-iris:predict HTTP/1.1\r\nHost: x\r\n"
+               b"Transfer-Encoding: chunked\r\n\r\n" + b"%x\r\n" % 10 + body[:10] + b"\r\n" +
+               b"%x;ext=1\r\n" % (len(body) - 10) + body[10:] + b"\r\n0\r\n\r\n")
+    close = req.replace(b"Host: x\r\n", b"Host: x\r\nConnection: close\r\n")
+    http10 = req.replace(b"HTTP/1.1\r\n", b"HTTP/1.0\r\n", 1)
+    cases = [
+        b"GARBAGE\r\n\r\n",
+        b"GET / HTTP/1.1 extra\r\n\r\n",
+        b"POST /v1/models/xgboost-iris:predict HTTP/1.1\r\nContent-Length: abc\r\n\r\n",
+        b"POST /v1/models/xgboost-iris:predict HTTP/1.1\r\nContent-Length: 999999999999\r\n\r\n",
+        chunked + close,          # a chunked request, then one that closes
+        req + req + close,        # three pipelined requests on one connection
+        http10,                   # HTTP/1.0: no keep-alive
+        close,
+    ]
+    try:
+        for data in cases:
+            a = _raw(nat.port, data, timeout=3)
+            b = _raw(py.port, data, timeout=3)
+            assert _norm(a) == _norm(b), (data[:60], a[:300], b[:300])
+            assert a.startswith(b"HTTP/1.1 ")
+    finally:
+        nat.stop()
+        py.stop()
+
+
+def test_concurrent_connections_share_batches(golden, tmp_path):
+    """Many connections at once: one batch answers several requests (one
+    batchId), every answer is the evaluator's for its own rows."""
+    import threading
+    from sklearn.datasets import load_iris
+    nat, py = _servers(golden, tmp_path, lat=20)
+    X = load_iris()["data"]
+    model = _xgb_model(golden, tmp_path / "ref")
+    out = [None] * 48
+    start = threading.Barrier(48)
+
+    def one(i):
+        rows = X[i:i + 1 + i % 3].tolist()
+        start.wait()
+        out[i] = (rows, nat.fetch("/v1/models/xgboost-iris:predict", "POST",
+                                  json.dumps({"instances": rows}).encode()))
+    th = [threading.Thread(target=one, args=(i,)) for i in range(48)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=30)
+    try:
+        ids = set()
+        for rows, (code, _, body) in out:
+            assert code == 200
+            res = json.loads(body)
+            ids.add(res["batchId"])
+            want = model.predict({"instances": rows})["predictions"]
+            assert res["predictions"] == want
+        assert len(ids) < 48
+    finally:
+        nat.stop()
+        py.stop()
+
+
+def test_reload_moves_the_route_to_the_new_batcher(golden, tmp_path):
+    """A reload through the repository route (/v2/repository/models/<m>/load)
+    retires the model's batchers: the native route is removed before its
+    batcher stops, the next request goes through the application, which makes
+    the new model's batcher, and the route comes back on it."""
+    from kfserving_amd.kfserving.kfmodel_repository import KFModelRepository
+
+    class Repo(KFModelRepository):
+        def load(self, name):
+            self.update(_xgb_model(golden, tmp_path / f"reload{len(loads)}"))
+            loads.append(name)
+            return True
+    loads = []
+    srv = KFServer(max_batchsize=64, max_latency_ms=3, registered_models=Repo())
+    srv.register_model(_xgb_model(golden, tmp_path / "first"))
+    nat = _Running(srv)
+    time.sleep(0.2)
+    body = b'{"instances": [[6.8, 2.8, 4.8, 1.4]]}'
+    try:
+        fe = srv.front_end
+        m0 = srv.registered_models.get_model("xgboost-iris")
+        first = nat.fetch("/v1/models/xgboost-iris:predict", "POST", body)
+        code, _, out = nat.fetch("/v2/repository/models/xgboost-iris/load", "POST", b"")
+        assert code == 200 and loads == ["xgboost-iris"]
+        assert "xgboost-iris" not in fe.routes
+        m1 = srv.registered_models.get_model("xgboost-iris")
+        assert m1 is not m0
+        code, _, out = nat.fetch("/v1/models/xgboost-iris:predict", "POST", body)
+        assert code == 200 and _norm(out) == _norm(first[2])
+        nb = fe.app._batchers[("xgboost-iris", "instances")]
+        assert nb.model is m1 and fe.routes["xgboost-iris"].value == nb._nb._h.value
+        n0 = fe.stats()["native_requests"]
+        assert nat.fetch("/v1/models/xgboost-iris:predict", "POST", body)[0] == 200
+        assert fe.stats()["native_requests"] == n0 + 1
+    finally:
+        nat.stop()
