@@ -95,8 +95,9 @@ struct IoThread {
   int idx = 0;
   int ep = -1, wake = -1;
   std::thread th;
-  std::mutex mu;                 // done
+  std::mutex mu;                 // done, new_fds
   std::deque<Done> done;
+  std::vector<int> new_fds;      // connections another thread accepted for this one
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;   // this thread only
   uint64_t next_id = 1;
 };
@@ -124,6 +125,7 @@ struct Server {
   std::atomic<bool> stop{false};
   std::atomic<int64_t> n_conn{0}, n_native{0}, n_python{0}, n_bad{0};
   std::deque<RouteCtx> ctxs;          // stable addresses, freed with the server
+  std::atomic<uint64_t> next_thread{0};   // round robin of accepted connections
   bool started = false;
 };
 
@@ -669,31 +671,50 @@ void on_readable(IoThread& t, Conn* c) {
   process(t, c);
 }
 
-void accept_all(IoThread& t) {
+// a connection joins thread t: registered in its epoll set, then read
+void adopt(IoThread& t, int fd) {
   Server& s = *t.srv;
-  for (;;) {
-    const int fd = accept4(s.cfg.listen_fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
-    if (fd < 0) {
-      if (errno == EINTR) continue;
-      return;   // EAGAIN: another thread or process took it
-    }
-    const int one = 1;
-    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-    auto c = std::make_unique<Conn>();
-    c->id = t.next_id++;
-    c->fd = fd;
-    epoll_event ev{};
-    ev.events = EPOLLIN | EPOLLRDHUP | EPOLLET;
-    ev.data.u64 = c->id;
-    if (epoll_ctl(t.ep, EPOLL_CTL_ADD, fd, &ev) != 0) {
-      close(fd);
-      continue;
-    }
-    Conn* cp = c.get();
-    t.conns.emplace(c->id, std::move(c));
-    s.n_conn.fetch_add(1);
-    on_readable(t, cp);
+  auto c = std::make_unique<Conn>();
+  c->id = t.next_id++;
+  c->fd = fd;
+  epoll_event ev{};
+  ev.events = EPOLLIN | EPOLLRDHUP | EPOLLET;
+  ev.data.u64 = c->id;
+  if (epoll_ctl(t.ep, EPOLL_CTL_ADD, fd, &ev) != 0) {
+    close(fd);
+    return;
   }
+  Conn* cp = c.get();
+  t.conns.emplace(c->id, std::move(c));
+  s.n_conn.fetch_add(1);
+  on_readable(t, cp);
+}
+
+// One connection per wake-up: with EPOLLEXCLUSIVE the next pending one wakes
+// another waiter (another worker process's threads included), so a burst of
+// connects spreads over the processes.  Inside this process the connections
+// go round robin over the IO threads (the request bodies' JSON parse is the
+// per-request cost an IO thread pays).
+void accept_one(IoThread& t) {
+  Server& s = *t.srv;
+  int fd;
+  do {
+    fd = accept4(s.cfg.listen_fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+  } while (fd < 0 && errno == EINTR);
+  if (fd < 0) return;   // EAGAIN: another thread or process took it
+  const int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  const size_t to = static_cast<size_t>(s.next_thread.fetch_add(1)) % s.io.size();
+  if (to == static_cast<size_t>(t.idx)) {
+    adopt(t, fd);
+    return;
+  }
+  IoThread& o = *s.io[to];
+  {
+    std::lock_guard<std::mutex> lk(o.mu);
+    o.new_fds.push_back(fd);
+  }
+  signal_fd(o.wake);
 }
 
 void io_main(IoThread* tp) {
@@ -701,18 +722,22 @@ void io_main(IoThread* tp) {
   Server& s = *t.srv;
   epoll_event evs[256];
   std::deque<Done> local;
+  std::vector<int> fds;
   while (!s.stop.load()) {
     const int n = epoll_wait(t.ep, evs, 256, 200);
     for (int i = 0; i < n; ++i) {
       const uint64_t key = evs[i].data.u64;
       if (key == kListen) {
-        accept_all(t);
+        accept_one(t);
       } else if (key == kWake) {
         drain_fd(t.wake);
         {
           std::lock_guard<std::mutex> lk(t.mu);
           local.swap(t.done);
+          fds.swap(t.new_fds);
         }
+        for (const int fd : fds) adopt(t, fd);
+        fds.clear();
         for (Done& d : local) on_done(t, d);
         local.clear();
       } else {
@@ -930,6 +955,7 @@ int kh_destroy(void* h) {
   }
   for (RouteCtx* c : live) detach(c);
   for (auto& t : s->io) {
+    for (const int fd : t->new_fds) close(fd);
     for (auto& kv : t->conns)
       if (kv.second->fd >= 0) close(kv.second->fd);
     t->conns.clear();

@@ -1,0 +1,64 @@
+"""The native HTTP front end (include/kfhttp.h) in front of the GPU: xgbserver
+with the C2 forest (500 depth-8 trees, 28 features) answers batched v1
+:predict requests natively through the native batcher and libtreeinfer; the
+bytes of every answer equal those of the asyncio server (KF_NATIVE_HTTP off)
+on the same requests, and the probabilities are the oracle's.  The CPU twin
+is tests/test_native_http.py."""
+import json
+import os
+import re
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from kfserving_amd.kfserving import KFServer
+from tests.test_server import _Running
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+pytestmark = pytest.mark.gpu
+
+
+def _norm(b: bytes) -> bytes:
+    return re.sub(rb'"batchId": "[0-9a-f-]{36}"', b'"batchId": "ID"', b)
+
+
+def test_native_http_c2_bytes_equal_python_server(tmp_path):
+    import bench_serving as bs
+    from kfserving_amd.xgbserver import XGBoostModel
+    from oracle import xgb_ref
+    bs.write_c2_model(str(tmp_path))
+    runs = []
+    for native in (True, False):
+        m = XGBoostModel("model", str(tmp_path), 1)
+        assert m.load()
+        srv = KFServer(max_batchsize=65536, max_latency_ms=3)
+        srv.native_http = native
+        srv.register_model(m)
+        runs.append(_Running(srv))
+    time.sleep(0.5)
+    nat, py = runs
+    ref = xgb_ref.read_xgb_binary(os.path.join(str(tmp_path), "model.bst"))
+    rng = np.random.default_rng(8)
+    try:
+        assert nat.server.front_end is not None and "model" in nat.server.front_end.routes
+        for i in range(24):
+            X = rng.standard_normal((int(rng.integers(1, 65)), 28)).astype(np.float32)
+            X[rng.random(X.shape) < 0.05] = 0.0          # DMatrix(list): missing
+            body = json.dumps({"instances": X.tolist()}).encode()
+            a = nat.fetch("/v1/models/model:predict", "POST", body)
+            b = py.fetch("/v1/models/model:predict", "POST", body)
+            assert a[0] == b[0] == 200 and a[1] == b[1]
+            assert _norm(a[2]) == _norm(b[2])
+            got = np.asarray(json.loads(a[2])["predictions"])
+            Xo = X.copy()
+            Xo[X == 0] = np.nan
+            np.testing.assert_allclose(got, xgb_ref.predict(ref, Xo), rtol=1e-5, atol=0)
+        st = nat.server.front_end.stats()
+        assert st["native_requests"] >= 24
+    finally:
+        nat.stop()
+        py.stop()
