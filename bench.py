@@ -147,6 +147,10 @@ def parse_args(argv=None):
                         "exceeds the 256 MB Infinity Cache)")
     p.add_argument("--host-rows", type=int, default=8_000_000,
                    help="rows of the host-to-host (PCIe-inclusive) C2 leg (0 = skip)")
+    p.add_argument("--c5-http-qps", default="20000,60000,100000",
+                   help="C5 over HTTP: offered req/s of the points (empty: skip); rank 0, "
+                        "after the GPU legs, a server of one worker per GPU")
+    p.add_argument("--c5-http-seconds", type=float, default=4.0)
     p.add_argument("--no-tree-shard", action="store_true",
                    help="skip the tree-sharded C2 leg (every rank a slice of the trees, "
                         "partial margins summed by one reduce: RCCL over xGMI at N > 1)")
@@ -642,6 +646,43 @@ def native_batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_laten
                     "(host buffers), arrivals submitted by a native thread (kb_loadgen), 1 GPU, "
                     "no HTTP/JSON",
             "_lat_ms": lat_ms}
+
+
+def c5_http_leg(args, world):
+    """BASELINE config C5 as named, over HTTP: xgbserver with the C2 forest
+    (`python -m kfserving_amd.xgbserver`, --max_batchsize 65536
+    --max_latency_ms 5) behind the native HTTP front end and native batcher,
+    one worker process per GPU of the job (worker i drives GPU i), 4,096
+    keep-alive connections from the C load generator (scripts/loadgen.c:
+    open-loop Poisson arrivals of U{1..64}-row v1 :predict bodies, latency
+    from the scheduled arrival).  Run on rank 0 after every rank's GPU legs;
+    the load generator is one epoll thread, so the offered rates are totals
+    for the node, not per GPU."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_serving as bs
+    env = dict(os.environ)
+    if world == 1:
+        env["TREEINFER_DEVICES"] = str(torch.cuda.current_device())
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+              "MASTER_PORT", "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    qps = [float(q) for q in args.c5_http_qps.split(",") if q.strip()]
+    io = max(2, 8 // world)
+    try:
+        pts = bs.serve_and_measure(qps, workers=world, io_threads=io,
+                                   duration=args.c5_http_seconds, warmup=1.5, conns=4096,
+                                   port=18090 + (os.getpid() % 500), env=env)
+    except Exception as e:   # reported, not fatal: the headline stands without it
+        return {"error": str(e)[-500:]}
+    keep = ("offered_qps", "req_per_s", "rows_per_s", "p50_ms", "p90_ms", "p99_ms", "max_ms",
+            "requests", "lost", "non200", "conn_errors")
+    return {"devices": world, "workers": world, "io_threads_per_worker": io,
+            "conns": 4096, "rows_per_request": "U{1..64}", "max_batch_size": 65536,
+            "max_latency_ms": 5, "model": "C2 (500 x depth 8, 28 features), xgbserver",
+            "path": "HTTP/1.1 keep-alive -> native front end (kfhttp.h) -> native batcher "
+                    "(kfbatch.h) -> ti_predict (host buffers)",
+            "points": [{k: p.get(k) for k in keep} for p in pts]}
 
 
 def tree_shard_leg(forest, dev, rows, args, world, rank, local_rank, device, dev_sync,
@@ -1171,6 +1212,9 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
         dist.destroy_process_group()
     if rank != 0:
         return None
+    c5_http = None
+    if args.c5_http_qps and device != "cpu":
+        c5_http = c5_http_leg(args, world)
     cpu = None
     if not args.no_cpu_baseline:
         cpu = cpu_baseline(trees, ti, X_host, args.cpu_seconds)
@@ -1219,6 +1263,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             "nan_variant": nan_variant,
             "host_pipeline": host_pipeline,
             "tree_shard": tree_shard,
+            "c5_http": c5_http,
         }
         line.update(configs)
     return line

@@ -59,7 +59,7 @@ parser.add_argument('--max_batchsize', default=0, type=int,
                     help='Enable the in-process batcher with this many rows per batch (0 = off).')
 parser.add_argument('--max_latency_ms', default=5000, type=int,
                     help='Batcher flush latency in milliseconds.')
-parser.add_argument('--http_io_threads', default=2, type=int,
+parser.add_argument('--http_io_threads', default=4, type=int,
                     help='IO threads of the native HTTP front end per worker process.')
 parser.add_argument('--no_fast_json', action='store_true',
                     help='Decode every body with json.loads (no native v1 parser).')

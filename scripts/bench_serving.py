@@ -96,6 +96,66 @@ def warm(port, n_feat, n=20):
             raise RuntimeError(f"warm-up predict returned {r.status}")
 
 
+def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.0, conns=4096,
+                      port=18080, model="c2", max_batch=65536, max_latency_ms=5, env=None):
+    """Start the server, drive it with the C load generator at each offered
+    rate in turn, stop it; one result dict per rate."""
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    resource.setrlimit(resource.RLIMIT_NOFILE, (hard, hard))
+    n_feat = 28
+    tmp = tempfile.mkdtemp()
+    bodies = os.path.join(tmp, "bodies.bin")
+    write_bodies(bodies, n_feat, 8, seed=3)
+    env = dict(os.environ if env is None else env)
+    if model == "c2":
+        write_c2_model(tmp)
+        cmd = [sys.executable, "-m", "kfserving_amd.xgbserver", "--model_dir", tmp,
+               "--model_name", "model", "--http_port", str(port),
+               "--workers", str(workers), "--max_batchsize", str(max_batch),
+               "--max_latency_ms", str(max_latency_ms), "--http_io_threads", str(io_threads)]
+    else:
+        code = DUMMY_SERVER % {"root": ROOT, "port": port, "workers": workers,
+                               "mbs": max_batch, "lat": max_latency_ms}
+        cmd = [sys.executable, "-c", code]
+    server = subprocess.Popen(cmd, cwd=ROOT, env=env, start_new_session=True,
+                              stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "server.log"), "w"))
+    results = []
+    try:
+        if not wait_ready(port):
+            raise RuntimeError("server did not become ready: " +
+                               open(os.path.join(tmp, "server.log")).read()[-2000:])
+        warm(port, n_feat)
+        for q in qps_list:
+            out = subprocess.run([LOADGEN, "--port", str(port), "--conns", str(conns),
+                                  "--qps", str(q), "--duration", str(duration),
+                                  "--warmup", str(warmup), "--bodies", bodies,
+                                  "--path", "/v1/models/model:predict"],
+                                 capture_output=True, text=True, timeout=duration * 3 + 120)
+            if out.returncode != 0:
+                raise RuntimeError(f"loadgen failed: {out.stderr[-2000:]}")
+            res = json.loads(out.stdout)
+            res.update({"config": "C5 dynamic batching: v1 :predict over HTTP, KFServer "
+                                  "in-process batcher", "model": model,
+                        "workers": workers, "max_batch_size": max_batch,
+                        "max_latency_ms": max_latency_ms,
+                        "native_http": env.get("KF_NATIVE_HTTP", "1") != "0",
+                        "native_batcher": env.get("KF_NATIVE_BATCHER", "1") != "0",
+                        "io_threads": io_threads,
+                        "gpus_visible": env.get("TREEINFER_DEVICES", "all")})
+            results.append(res)
+            print(json.dumps(res), flush=True)
+    finally:
+        try:
+            os.killpg(server.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+        try:
+            server.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            os.killpg(server.pid, signal.SIGKILL)
+    return results
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--qps", default="5000,10000,20000")
@@ -111,58 +171,9 @@ def main():
                    help="native HTTP front end IO threads per worker (KF_NATIVE_HTTP=0: "
                         "the asyncio server)")
     args = p.parse_args()
-    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
-    resource.setrlimit(resource.RLIMIT_NOFILE, (hard, hard))
-    n_feat = 28
-    tmp = tempfile.mkdtemp()
-    bodies = os.path.join(tmp, "bodies.bin")
-    write_bodies(bodies, n_feat, 8, seed=3)
-    env = dict(os.environ)
-    if args.model == "c2":
-        write_c2_model(tmp)
-        cmd = [sys.executable, "-m", "kfserving_amd.xgbserver", "--model_dir", tmp,
-               "--model_name", "model", "--http_port", str(args.port),
-               "--workers", str(args.workers), "--max_batchsize", str(args.max_batch),
-               "--max_latency_ms", str(args.max_latency_ms),
-               "--http_io_threads", str(args.io_threads)]
-    else:
-        code = DUMMY_SERVER % {"root": ROOT, "port": args.port, "workers": args.workers,
-                               "mbs": args.max_batch, "lat": args.max_latency_ms}
-        cmd = [sys.executable, "-c", code]
-    server = subprocess.Popen(cmd, cwd=ROOT, env=env, start_new_session=True,
-                              stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "server.log"), "w"))
-    try:
-        if not wait_ready(args.port):
-            raise RuntimeError("server did not become ready: " +
-                               open(os.path.join(tmp, "server.log")).read()[-2000:])
-        warm(args.port, n_feat)
-        for q in [float(x) for x in args.qps.split(",")]:
-            out = subprocess.run([LOADGEN, "--port", str(args.port), "--conns", str(args.conns),
-                                  "--qps", str(q), "--duration", str(args.duration),
-                                  "--warmup", str(args.warmup), "--bodies", bodies,
-                                  "--path", "/v1/models/model:predict"],
-                                 capture_output=True, text=True, timeout=args.duration * 3 + 120)
-            if out.returncode != 0:
-                raise RuntimeError(f"loadgen failed: {out.stderr[-2000:]}")
-            res = json.loads(out.stdout)
-            res.update({"config": "C5 dynamic batching: v1 :predict over HTTP, KFServer "
-                                  "in-process batcher", "model": args.model,
-                        "workers": args.workers, "max_batch_size": args.max_batch,
-                        "max_latency_ms": args.max_latency_ms,
-                        "native_http": os.environ.get("KF_NATIVE_HTTP", "1") != "0",
-                        "native_batcher": os.environ.get("KF_NATIVE_BATCHER", "1") != "0",
-                        "io_threads": args.io_threads,
-                        "gpus_visible": os.environ.get("TREEINFER_DEVICES", "all")})
-            print(json.dumps(res), flush=True)
-    finally:
-        try:
-            os.killpg(server.pid, signal.SIGTERM)
-        except ProcessLookupError:
-            pass
-        try:
-            server.wait(timeout=20)
-        except subprocess.TimeoutExpired:
-            os.killpg(server.pid, signal.SIGKILL)
+    serve_and_measure([float(x) for x in args.qps.split(",")], args.workers, args.io_threads,
+                      args.duration, args.warmup, args.conns, args.port, args.model,
+                      args.max_batch, args.max_latency_ms)
 
 
 if __name__ == "__main__":
