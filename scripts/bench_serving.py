@@ -97,7 +97,8 @@ def warm(port, n_feat, n=20):
 
 
 def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.0, conns=4096,
-                      port=18080, model="c2", max_batch=65536, max_latency_ms=5, env=None):
+                      port=18080, model="c2", max_batch=65536, max_latency_ms=5, env=None,
+                      ready_timeout=180):
     """Start the server, drive it with the C load generator at each offered
     rate in turn, stop it; one result dict per rate."""
     soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
@@ -121,7 +122,7 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
                               stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "server.log"), "w"))
     results = []
     try:
-        if not wait_ready(port):
+        if not wait_ready(port, ready_timeout):
             raise RuntimeError("server did not become ready: " +
                                open(os.path.join(tmp, "server.log")).read()[-2000:])
         warm(port, n_feat)
