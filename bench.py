@@ -655,9 +655,9 @@ def c5_http_leg(args, world):
     one worker process per GPU of the job (worker i drives GPU i), 4,096
     keep-alive connections from the C load generator (scripts/loadgen.c:
     open-loop Poisson arrivals of U{1..64}-row v1 :predict bodies, latency
-    from the scheduled arrival).  Run on rank 0 after every rank's GPU legs;
-    the load generator is one epoll thread, so the offered rates are totals
-    for the node, not per GPU."""
+    from the scheduled arrival; 4 threads, each its own epoll loop).  Run on
+    rank 0 after every rank's GPU legs; the offered rates are totals for the
+    node, not per GPU."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import bench_serving as bs
@@ -673,13 +673,14 @@ def c5_http_leg(args, world):
         pts = bs.serve_and_measure(qps, workers=world, io_threads=io,
                                    duration=args.c5_http_seconds, warmup=1.5, conns=4096,
                                    port=18090 + (os.getpid() % 500), env=env,
-                                   ready_timeout=90)
+                                   ready_timeout=90, loadgen_threads=4)
     except Exception as e:   # reported, not fatal: the headline stands without it
         return {"error": str(e)[-500:]}
     keep = ("offered_qps", "req_per_s", "rows_per_s", "p50_ms", "p90_ms", "p99_ms", "max_ms",
             "requests", "lost", "non200", "conn_errors")
     return {"devices": world, "workers": world, "io_threads_per_worker": io,
-            "conns": 4096, "rows_per_request": "U{1..64}", "max_batch_size": 65536,
+            "conns": 4096, "loadgen_threads": 4, "rows_per_request": "U{1..64}",
+            "max_batch_size": 65536,
             "max_latency_ms": 5, "model": "C2 (500 x depth 8, 28 features), xgbserver",
             "path": "HTTP/1.1 keep-alive -> native front end (kfhttp.h) -> native batcher "
                     "(kfbatch.h) -> ti_predict (host buffers)",

@@ -98,7 +98,7 @@ def warm(port, n_feat, n=20):
 
 def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.0, conns=4096,
                       port=18080, model="c2", max_batch=65536, max_latency_ms=5, env=None,
-                      ready_timeout=180):
+                      ready_timeout=180, loadgen_threads=1):
     """Start the server, drive it with the C load generator at each offered
     rate in turn, stop it; one result dict per rate."""
     soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
@@ -130,6 +130,7 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
             out = subprocess.run([LOADGEN, "--port", str(port), "--conns", str(conns),
                                   "--qps", str(q), "--duration", str(duration),
                                   "--warmup", str(warmup), "--bodies", bodies,
+                                  "--threads", str(loadgen_threads),
                                   "--path", "/v1/models/model:predict"],
                                  capture_output=True, text=True, timeout=duration * 3 + 120)
             if out.returncode != 0:
@@ -141,7 +142,7 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
                         "max_latency_ms": max_latency_ms,
                         "native_http": env.get("KF_NATIVE_HTTP", "1") != "0",
                         "native_batcher": env.get("KF_NATIVE_BATCHER", "1") != "0",
-                        "io_threads": io_threads,
+                        "io_threads": io_threads, "loadgen_threads": loadgen_threads,
                         "gpus_visible": env.get("TREEINFER_DEVICES", "all")})
             results.append(res)
             print(json.dumps(res), flush=True)
@@ -168,13 +169,16 @@ def main():
     p.add_argument("--model", default="c2", choices=["c2", "dummy"])
     p.add_argument("--max-batch", type=int, default=65536)
     p.add_argument("--max-latency-ms", type=int, default=5)
+    p.add_argument("--loadgen-threads", type=int, default=1,
+                   help="load generator threads (each its own epoll loop and share of the "
+                        "connections and rate)")
     p.add_argument("--io-threads", type=int, default=2,
                    help="native HTTP front end IO threads per worker (KF_NATIVE_HTTP=0: "
                         "the asyncio server)")
     args = p.parse_args()
     serve_and_measure([float(x) for x in args.qps.split(",")], args.workers, args.io_threads,
                       args.duration, args.warmup, args.conns, args.port, args.model,
-                      args.max_batch, args.max_latency_ms)
+                      args.max_batch, args.max_latency_ms, loadgen_threads=args.loadgen_threads)
 
 
 if __name__ == "__main__":

@@ -7,7 +7,10 @@
 // scripts/bench_serving.py).  A request goes to an idle keep-alive
 // connection (--conns of them, all opened up front); when none is idle it
 // waits in a FIFO, and its latency still counts from its scheduled arrival,
-// so queueing shows up in the tail.  One epoll loop, no threads.
+// so queueing shows up in the tail.  --threads T splits the connections and
+// the rate over T threads, each its own epoll loop and Poisson process (the
+// sum of independent Poisson processes is one at the total rate), for rates
+// one loop cannot drive.
 //
 // Output: one JSON line with p50/p90/p99/max latency (ms) over the requests
 // scheduled after --warmup seconds, completed requests and rows per second.
@@ -18,6 +21,7 @@
 #include <math.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -52,7 +56,7 @@ static double now_s(void) {
   return t.tv_sec + t.tv_nsec * 1e-9;
 }
 
-static uint64_t rng_state = 88172645463325252ULL;
+static __thread uint64_t rng_state = 88172645463325252ULL;
 static uint64_t xr(void) {
   rng_state ^= rng_state << 13;
   rng_state ^= rng_state >> 7;
@@ -60,6 +64,24 @@ static uint64_t xr(void) {
   return rng_state;
 }
 static double urand(void) { return (xr() >> 11) * (1.0 / 9007199254740992.0); }
+
+typedef struct {      // one thread's share of the load and its results
+  uint64_t seed;
+  int nconn;
+  double qps, dur, warm, t0;
+  const Req* reqs;
+  uint32_t nv;
+  struct sockaddr_in sa;
+  int64_t nj;
+  double* sched;
+  const Req** which;
+  double* lat;
+  int* status;
+  int opened;
+  int64_t errors;
+} Share;
+
+static void* run_share(void* arg);
 
 static int cmp_d(const void* a, const void* b) {
   double x = *(const double*)a, y = *(const double*)b;
@@ -72,51 +94,15 @@ static const char* arg(int argc, char** argv, const char* k, const char* d) {
   return d;
 }
 
-int main(int argc, char** argv) {
-  const char* host = arg(argc, argv, "--host", "127.0.0.1");
-  int port = atoi(arg(argc, argv, "--port", "8080"));
-  const char* path = arg(argc, argv, "--path", "/v1/models/model:predict");
-  int nconn = atoi(arg(argc, argv, "--conns", "4096"));
-  double qps = atof(arg(argc, argv, "--qps", "10000"));
-  double dur = atof(arg(argc, argv, "--duration", "10"));
-  double warm = atof(arg(argc, argv, "--warmup", "2"));
-  const char* bodies = arg(argc, argv, "--bodies", "bodies.bin");
-  rng_state ^= (uint64_t)atoll(arg(argc, argv, "--seed", "7")) * 0x9E3779B97F4A7C15ULL;
-
-  struct rlimit rl;
-  getrlimit(RLIMIT_NOFILE, &rl);
-  rl.rlim_cur = rl.rlim_max;
-  setrlimit(RLIMIT_NOFILE, &rl);
-  if ((rlim_t)nconn + 64 > rl.rlim_cur) nconn = (int)rl.rlim_cur - 64;
-
-  // bodies file: u32 n_variants, then for rows 1..64, n_variants x (u32 len, bytes)
-  FILE* f = fopen(bodies, "rb");
-  if (!f) { perror("bodies"); return 2; }
-  uint32_t nv;
-  if (fread(&nv, 4, 1, f) != 1 || nv == 0) { fprintf(stderr, "bad bodies file\n"); return 2; }
-  Req* reqs = calloc((size_t)MAXR * nv, sizeof(Req));
-  for (int r = 1; r <= MAXR; ++r)
-    for (uint32_t v = 0; v < nv; ++v) {
-      uint32_t bl;
-      if (fread(&bl, 4, 1, f) != 1) { fprintf(stderr, "short bodies file\n"); return 2; }
-      char* body = malloc(bl);
-      if (fread(body, 1, bl, f) != bl) { fprintf(stderr, "short bodies file\n"); return 2; }
-      Req* q = &reqs[(r - 1) * nv + v];
-      char hdr[512];
-      int hl = snprintf(hdr, sizeof hdr,
-                        "POST %s HTTP/1.1\r\nHost: %s:%d\r\nContent-Type: application/json\r\n"
-                        "Content-Length: %u\r\n\r\n", path, host, port, bl);
-      q->req = malloc((size_t)hl + bl);
-      memcpy(q->req, hdr, (size_t)hl);
-      memcpy(q->req + hl, body, bl);
-      q->len = hl + (int)bl;
-      q->rows = r;
-      free(body);
-    }
-  fclose(f);
-
+static void* run_share(void* arg) {
+  Share* z = (Share*)arg;
+  rng_state = z->seed;
+  const double qps = z->qps, dur = z->dur, warm = z->warm;
+  const int nconn = z->nconn;
+  const uint32_t nv = z->nv;
+  const struct sockaddr_in sa = z->sa;
   // schedule
-  int64_t njobs = (int64_t)(qps * (dur + warm) * 1.02) + 16;
+  int64_t njobs = (int64_t)(qps * (dur + warm) * 1.05) + 64;
   double* sched = malloc(sizeof(double) * njobs);
   const Req** which = malloc(sizeof(Req*) * njobs);
   double* lat = malloc(sizeof(double) * njobs);
@@ -128,16 +114,11 @@ int main(int argc, char** argv) {
     if (t >= dur + warm) break;
     sched[nj] = t;
     int r = 1 + (int)(xr() % MAXR);
-    which[nj] = &reqs[(r - 1) * nv + (xr() % nv)];
+    which[nj] = &z->reqs[(r - 1) * nv + (xr() % nv)];
     lat[nj] = -1;
     ++nj;
   }
 
-  struct sockaddr_in sa;
-  memset(&sa, 0, sizeof sa);
-  sa.sin_family = AF_INET;
-  sa.sin_port = htons((uint16_t)port);
-  inet_pton(AF_INET, host, &sa.sin_addr);
   int ep = epoll_create1(0);
   Conn* cs = calloc((size_t)nconn, sizeof(Conn));
   int opened = 0;
@@ -155,14 +136,15 @@ int main(int argc, char** argv) {
     epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
     ++opened;
   }
-  if (opened == 0) { fprintf(stderr, "could not connect\n"); return 3; }
+  z->opened = opened;
+  if (opened == 0) return NULL;
   int* idle = malloc(sizeof(int) * opened);
   int nidle = 0;
   for (int i = opened - 1; i >= 0; --i) idle[nidle++] = i;
   int64_t* fifo = malloc(sizeof(int64_t) * (size_t)nj);
   int64_t fh = 0, ft = 0;
 
-  const double t0 = now_s() + 0.01;
+  const double t0 = z->t0;
   int64_t next = 0, done = 0, errors = 0;
   double end_t = t0 + dur + warm + 30.0;   // drain limit
 
@@ -245,19 +227,109 @@ int main(int argc, char** argv) {
     }
   }
 
+  z->nj = nj;
+  z->sched = sched;
+  z->which = which;
+  z->lat = lat;
+  z->status = status;
+  z->errors = errors;
+  for (int i = 0; i < opened; ++i)
+    if (cs[i].fd >= 0) close(cs[i].fd);
+  return NULL;
+}
+
+int main(int argc, char** argv) {
+  const char* host = arg(argc, argv, "--host", "127.0.0.1");
+  int port = atoi(arg(argc, argv, "--port", "8080"));
+  const char* path = arg(argc, argv, "--path", "/v1/models/model:predict");
+  int nconn = atoi(arg(argc, argv, "--conns", "4096"));
+  double qps = atof(arg(argc, argv, "--qps", "10000"));
+  double dur = atof(arg(argc, argv, "--duration", "10"));
+  double warm = atof(arg(argc, argv, "--warmup", "2"));
+  const char* bodies = arg(argc, argv, "--bodies", "bodies.bin");
+
+  struct rlimit rl;
+  getrlimit(RLIMIT_NOFILE, &rl);
+  rl.rlim_cur = rl.rlim_max;
+  setrlimit(RLIMIT_NOFILE, &rl);
+  if ((rlim_t)nconn + 64 > rl.rlim_cur) nconn = (int)rl.rlim_cur - 64;
+
+  // bodies file: u32 n_variants, then for rows 1..64, n_variants x (u32 len, bytes)
+  FILE* f = fopen(bodies, "rb");
+  if (!f) { perror("bodies"); return 2; }
+  uint32_t nv;
+  if (fread(&nv, 4, 1, f) != 1 || nv == 0) { fprintf(stderr, "bad bodies file\n"); return 2; }
+  Req* reqs = calloc((size_t)MAXR * nv, sizeof(Req));
+  for (int r = 1; r <= MAXR; ++r)
+    for (uint32_t v = 0; v < nv; ++v) {
+      uint32_t bl;
+      if (fread(&bl, 4, 1, f) != 1) { fprintf(stderr, "short bodies file\n"); return 2; }
+      char* body = malloc(bl);
+      if (fread(body, 1, bl, f) != bl) { fprintf(stderr, "short bodies file\n"); return 2; }
+      Req* q = &reqs[(r - 1) * nv + v];
+      char hdr[512];
+      int hl = snprintf(hdr, sizeof hdr,
+                        "POST %s HTTP/1.1\r\nHost: %s:%d\r\nContent-Type: application/json\r\n"
+                        "Content-Length: %u\r\n\r\n", path, host, port, bl);
+      q->req = malloc((size_t)hl + bl);
+      memcpy(q->req, hdr, (size_t)hl);
+      memcpy(q->req + hl, body, bl);
+      q->len = hl + (int)bl;
+      q->rows = r;
+      free(body);
+    }
+  fclose(f);
+
+  int nthreads = atoi(arg(argc, argv, "--threads", "1"));
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > nconn) nthreads = nconn;
+  uint64_t seed0 = (uint64_t)atoll(arg(argc, argv, "--seed", "7"));
+  struct sockaddr_in sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons((uint16_t)port);
+  inet_pton(AF_INET, host, &sa.sin_addr);
+  Share* sh = calloc((size_t)nthreads, sizeof(Share));
+  pthread_t* th = calloc((size_t)nthreads, sizeof(pthread_t));
+  const double t0 = now_s() + 0.05 + 0.0005 * nconn;   // after every connect
+  for (int k = 0; k < nthreads; ++k) {
+    sh[k].seed = (88172645463325252ULL ^ (seed0 * 0x9E3779B97F4A7C15ULL)) + 0x632BE59BD9B4E019ULL * (uint64_t)k;
+    sh[k].nconn = nconn / nthreads + (k < nconn % nthreads);
+    sh[k].qps = qps / nthreads;
+    sh[k].dur = dur;
+    sh[k].warm = warm;
+    sh[k].t0 = t0;
+    sh[k].reqs = reqs;
+    sh[k].nv = nv;
+    sh[k].sa = sa;
+    pthread_create(&th[k], NULL, run_share, &sh[k]);
+  }
+  int opened = 0;
+  int64_t errors = 0, nj = 0;
+  for (int k = 0; k < nthreads; ++k) {
+    pthread_join(th[k], NULL);
+    opened += sh[k].opened;
+    errors += sh[k].errors;
+    nj += sh[k].nj;
+  }
+  if (opened == 0) { fprintf(stderr, "could not connect\n"); return 3; }
+
   // report requests scheduled after warmup
-  double* l = malloc(sizeof(double) * (size_t)nj);
+  double* l = malloc(sizeof(double) * (size_t)(nj + 1));
   int64_t m = 0, non200 = 0, rows = 0, lost = 0;
   double first = -1, last = 0;
-  for (int64_t i = 0; i < nj; ++i) {
-    if (sched[i] < warm) continue;
-    if (lat[i] < 0) { ++lost; continue; }
-    if (status[i] != 200) ++non200;
-    l[m++] = lat[i];
-    rows += which[i]->rows;
-    double fin = sched[i] + lat[i];
-    if (first < 0 || sched[i] < first) first = sched[i];
-    if (fin > last) last = fin;
+  for (int k = 0; k < nthreads; ++k) {
+    const Share* z = &sh[k];
+    for (int64_t i = 0; i < z->nj; ++i) {
+      if (z->sched[i] < warm) continue;
+      if (z->lat[i] < 0) { ++lost; continue; }
+      if (z->status[i] != 200) ++non200;
+      l[m++] = z->lat[i];
+      rows += z->which[i]->rows;
+      double fin = z->sched[i] + z->lat[i];
+      if (first < 0 || z->sched[i] < first) first = z->sched[i];
+      if (fin > last) last = fin;
+    }
   }
   qsort(l, (size_t)m, sizeof(double), cmp_d);
   double span = last - first > 0 ? last - first : 1;
