@@ -673,7 +673,7 @@ def c5_http_leg(args, world):
         pts = bs.serve_and_measure(qps, workers=world, io_threads=io,
                                    duration=args.c5_http_seconds, warmup=1.5, conns=4096,
                                    port=18090 + (os.getpid() % 500), env=env,
-                                   ready_timeout=90, loadgen_threads=4)
+                                   ready_timeout=90, loadgen_threads=4, echo=False)
     except Exception as e:   # reported, not fatal: the headline stands without it
         return {"error": str(e)[-500:]}
     keep = ("offered_qps", "req_per_s", "rows_per_s", "p50_ms", "p90_ms", "p99_ms", "max_ms",

@@ -98,7 +98,7 @@ def warm(port, n_feat, n=20):
 
 def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.0, conns=4096,
                       port=18080, model="c2", max_batch=65536, max_latency_ms=5, env=None,
-                      ready_timeout=180, loadgen_threads=1):
+                      ready_timeout=180, loadgen_threads=1, echo=True):
     """Start the server, drive it with the C load generator at each offered
     rate in turn, stop it; one result dict per rate."""
     soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
@@ -145,7 +145,8 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
                         "io_threads": io_threads, "loadgen_threads": loadgen_threads,
                         "gpus_visible": env.get("TREEINFER_DEVICES", "all")})
             results.append(res)
-            print(json.dumps(res), flush=True)
+            if echo:   # bench.py's leg prints nothing of its own (one JSON line)
+                print(json.dumps(res), flush=True)
     finally:
         try:
             os.killpg(server.pid, signal.SIGTERM)

@@ -8,6 +8,7 @@ import subprocess
 import sys
 import time
 
+import pytest
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -155,3 +156,18 @@ def test_headline_defaults_two_streams():
     import bench
     assert bench.parse_args([]).streams == 2
     assert bench.parse_args(["--streams", "1"]).streams == 1
+
+
+def test_http_leg_prints_nothing_of_its_own(capsys):
+    """bench.py's c5_http leg calls bench_serving.serve_and_measure with
+    echo=False: rank 0's stdout must stay the one JSON line (here with the
+    CPU echo model and a short load)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_serving as bs
+    if not os.path.exists(bs.LOADGEN):
+        pytest.skip("loadgen not built")
+    pts = bs.serve_and_measure([500.0], workers=1, io_threads=1, duration=0.5, warmup=0.2,
+                               conns=16, port=18000 + os.getpid() % 900, model="dummy",
+                               ready_timeout=60, loadgen_threads=2, echo=False)
+    assert len(pts) == 1 and pts[0]["completed"] > 0 and pts[0]["non200"] == 0
+    assert capsys.readouterr().out == ""
