@@ -39,8 +39,10 @@ def test_native_http_c2_bytes_equal_python_server(tmp_path):
         srv.native_http = native
         srv.register_model(m)
         runs.append(_Running(srv))
-    time.sleep(0.5)
     nat, py = runs
+    t0 = time.time()
+    while nat.server.front_end is None and time.time() - t0 < 60:
+        time.sleep(0.05)
     ref = xgb_ref.read_xgb_binary(os.path.join(str(tmp_path), "model.bst"))
     rng = np.random.default_rng(8)
     try:

@@ -68,8 +68,16 @@ def _servers(golden, tmp_path, **kw):
         srv.native_http = native
         srv.register_model(_xgb_model(golden, tmp_path / ("n" if native else "p")))
         out.append(_Running(srv))
-    time.sleep(0.2)
+    _wait_front_end(out[0])
     return out
+
+
+def _wait_front_end(running, timeout=30.0):
+    """serve() installs the native front end on the server's thread."""
+    t0 = time.time()
+    while running.server.front_end is None and time.time() - t0 < timeout:
+        time.sleep(0.02)
+    assert running.server.front_end is not None, "native front end did not start"
 
 
 def _raw(port, data: bytes, timeout=10.0) -> bytes:
@@ -244,7 +252,7 @@ def test_reload_moves_the_route_to_the_new_batcher(golden, tmp_path):
     srv = KFServer(max_batchsize=64, max_latency_ms=3, registered_models=Repo())
     srv.register_model(_xgb_model(golden, tmp_path / "first"))
     nat = _Running(srv)
-    time.sleep(0.2)
+    _wait_front_end(nat)
     body = b'{"instances": [[6.8, 2.8, 4.8, 1.4]]}'
     try:
         fe = srv.front_end
