@@ -69,9 +69,15 @@ int kh_create(const kh_config* cfg, void** out);
 /* Answer POST /v1/models/<model>:predict natively through `batcher` (a kb_*
  * handle whose rows have n_cols columns and out_width outputs of
  * out_elem_bytes (4: float32, 8: float64) each), converting each request's
- * float64 rows with kb_submit_convert's `transform`.  The server takes the
+ * float64 rows with kb_submit_convert's `transform` (low 8 bits; KH_CHECK_*
+ * flags above them).  The server takes the
  * batcher's done callback (kb_set_done_callback).  -1 if the model already
  * has a route. */
+#define KH_CHECK_F32_FINITE (1 << 8)  /* hand to the application a body with a value
+                                         that is +-inf after the float32 cast
+                                         (sklearn's check_array on X.astype(float32)) */
+#define KH_CHECK_NO_NAN     (1 << 9)  /* ... or holding a NaN (estimators without
+                                         missing-value support)                     */
 int kh_add_v1_predict(void* srv, const char* model, void* batcher, int32_t n_cols,
                       int32_t out_width, int32_t out_elem_bytes, int32_t transform);
 

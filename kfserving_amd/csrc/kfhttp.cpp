@@ -518,6 +518,9 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
     if (it == s.routes.end()) return false;
     route = it->second;
   }
+  // the plugin's input checks, as flags above the element rule: a request
+  // they would reject goes to the application, which answers its error
+  const int rule = route.transform & 0xFF;
   thread_local std::vector<double> xb;
   const size_t cap = (r.body.size() + 1) / 2;
   if (xb.size() < cap) xb.resize(cap);
@@ -526,6 +529,14 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
                          static_cast<int64_t>(xb.size()), &rows, &cols) != KF_PARSED ||
       rows <= 0 || cols != route.n_cols)
     return false;
+  if (route.transform & (KH_CHECK_F32_FINITE | KH_CHECK_NO_NAN)) {
+    const bool fin = route.transform & KH_CHECK_F32_FINITE, nonan = route.transform & KH_CHECK_NO_NAN;
+    for (int64_t i = 0; i < rows * cols; ++i) {
+      const double v = xb[static_cast<size_t>(i)];
+      if (nonan && std::isnan(v)) return false;
+      if (fin && std::isinf(static_cast<float>(v))) return false;
+    }
+  }
   c->route = route;
   c->rows = rows;
   c->keep = keep;
@@ -533,7 +544,7 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   c->busy = true;
   const uint64_t tag = KB_TAG_CALLBACK | (static_cast<uint64_t>(t.idx) << kThreadShift) | c->id;
   route.ctx->inflight.fetch_add(1);
-  if (kb_submit_convert(route.batcher, xb.data(), 1, rows, cols, route.transform, c->res.data(),
+  if (kb_submit_convert(route.batcher, xb.data(), 1, rows, cols, rule, c->res.data(),
                         tag) != KB_OK) {
     route.ctx->inflight.fetch_sub(1);
     c->busy = false;   // the batcher was retired meanwhile: the application answers

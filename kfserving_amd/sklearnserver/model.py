@@ -83,6 +83,17 @@ class SKLearnModel(GPUForestMixin, KFModel):  # pylint:disable=c-extension-no-me
             result = np.asarray(classes).take(result.astype(np.int64), axis=0)
         return result
 
+    @property
+    def native_v1_transform(self):
+        """The native HTTP route's element rule and checks (kfhttp.h): the
+        float32 cast, a value that overflows it or a NaN the estimator
+        rejects sends the request to predict's own checks; classifiers (label
+        mapping) keep the application's path."""
+        f = self._forest
+        if f is None or f.meta.get("classes") is not None:
+            return None
+        return (1 << 8) | (0 if f.meta.get("allow_nan", True) else (1 << 9))
+
     def native_rows(self, chunk, kind: str) -> np.ndarray:
         # the same checks for V2 tensors and instances (predict_tensor)
         X = chunk if kind == "inputs" else self.request_matrix({"instances": chunk})

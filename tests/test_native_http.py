@@ -272,3 +272,50 @@ def test_reload_moves_the_route_to_the_new_batcher(golden, tmp_path):
         assert fe.stats()["native_requests"] == n0 + 1
     finally:
         nat.stop()
+
+
+def test_sklearn_regressor_route_and_its_checks(golden, tmp_path):
+    """sklearnserver regressors get a native route too: the float32 cast,
+    and a body the model's own checks reject (a value beyond float32, an
+    infinity, a NaN for an estimator without missing-value support) is
+    answered by the application, byte for byte as the asyncio server."""
+    from kfserving_amd.sklearnserver import SKLearnModel
+
+    def model(sub, allow_nan=True):
+        d = tmp_path / sub
+        d.mkdir(parents=True)
+        shutil.copy(os.path.join(golden, "sk_rf_reg_model.npz"), str(d / "model.npz"))
+        m = SKLearnModel("sk", str(d))
+        assert m.load()
+        m._forest.meta["allow_nan"] = allow_nan
+        m.predict_matrix = lambda X, kind=OUT_PREDICT: canon_eval.predict(m._forest, X, kind)
+        return m
+    g = np.load(os.path.join(golden, "sk_rf_reg.npz"))
+    X = np.nan_to_num(g["X"][:6]).astype(np.float64)
+    F = X.shape[1]
+    for allow_nan in (True, False):
+        runs = []
+        for native in (True, False):
+            srv = KFServer(max_batchsize=64, max_latency_ms=3)
+            srv.native_http = native
+            srv.register_model(model(f"{allow_nan}{native}", allow_nan))
+            runs.append(_Running(srv))
+        nat, py = runs
+        _wait_front_end(nat)
+        try:
+            assert "sk" in nat.server.front_end.routes
+            bodies = [json.dumps({"instances": X[:k].tolist()}).encode() for k in (1, 3, 6)]
+            bad = X[:2].tolist()
+            bad[1][0] = 1e39
+            bodies.append(json.dumps({"instances": bad}).encode())
+            bodies.append(json.dumps({"instances": [[float("inf")] * F]}).encode())
+            bodies.append(json.dumps({"instances": [[float("nan")] + [0.5] * (F - 1)]}).encode())
+            for body in bodies:
+                a = nat.fetch("/v1/models/sk:predict", "POST", body)
+                b = py.fetch("/v1/models/sk:predict", "POST", body)
+                assert a[0] == b[0] and a[1] == b[1] and _norm(a[2]) == _norm(b[2]), body[:80]
+            st = nat.server.front_end.stats()
+            assert st["native_requests"] >= 3 and st["python_requests"] >= 2
+        finally:
+            nat.stop()
+            py.stop()
