@@ -482,7 +482,7 @@ std::string predict_route(const std::string& target) {
   return name;
 }
 
-void process(IoThread& t, Conn* c);
+bool process(IoThread& t, Conn* c);
 
 void hand_to_python(IoThread& t, Conn* c, Req& r, bool keep) {
   Server& s = *t.srv;
@@ -513,11 +513,22 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
     if (r.h.count(h)) return false;   // binary CloudEvents: the application's path
   Route route;
   {
+    // the reservation is taken under the route lock: kh_remove_route erases
+    // the route under it and then waits for every reservation, so the batcher
+    // cannot be destroyed between this lookup and the submit below
     std::lock_guard<std::mutex> lk(s.rmu);
     auto it = s.routes.find(name);
     if (it == s.routes.end()) return false;
     route = it->second;
+    route.ctx->inflight.fetch_add(1);
   }
+  struct Reservation {
+    RouteCtx* ctx;
+    bool held = true;
+    ~Reservation() {
+      if (held) ctx->inflight.fetch_sub(1);
+    }
+  } res{route.ctx};
   // the plugin's input checks, as flags above the element rule: a request
   // they would reject goes to the application, which answers its error
   const int rule = route.transform & 0xFF;
@@ -543,13 +554,12 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   c->res.assign(static_cast<size_t>(rows) * route.out_width * route.out_elem, 0);
   c->busy = true;
   const uint64_t tag = KB_TAG_CALLBACK | (static_cast<uint64_t>(t.idx) << kThreadShift) | c->id;
-  route.ctx->inflight.fetch_add(1);
   if (kb_submit_convert(route.batcher, xb.data(), 1, rows, cols, rule, c->res.data(),
                         tag) != KB_OK) {
-    route.ctx->inflight.fetch_sub(1);
     c->busy = false;   // the batcher was retired meanwhile: the application answers
     return false;
   }
+  res.held = false;    // native_done releases it with the completion
   s.n_native.fetch_add(1);
   return true;
 }
@@ -598,13 +608,14 @@ void answer_native(Conn* c, const kb_completion& d, const std::string& err) {
   std::vector<unsigned char>().swap(c->res);
 }
 
-void process(IoThread& t, Conn* c) {
+// parse and dispatch what is buffered; false if the connection was freed
+bool process(IoThread& t, Conn* c) {
   Server& s = *t.srv;
   while (!c->busy && c->fd >= 0 && !c->close_after) {
     if (c->in_off >= c->in.size()) {
       c->in.clear();
       c->in_off = 0;
-      return;
+      return true;
     }
     Req r;
     const Parse p = parse_request(c->in, c->in_off, s.cfg.max_body_bytes, &r);
@@ -613,7 +624,7 @@ void process(IoThread& t, Conn* c) {
         c->in.erase(0, c->in_off);
         c->in_off = 0;
       }
-      return;
+      return true;
     }
     if (p == Parse::kBad || p == Parse::kTooLarge) {
       if (p == Parse::kBad) append_error(c->out, 400, "Bad Request");
@@ -622,14 +633,14 @@ void process(IoThread& t, Conn* c) {
       c->close_after = true;
       c->in.clear();
       c->in_off = 0;
-      flush_out(t, c);
-      return;
+      return flush_out(t, c);
     }
     c->in_off = r.end;
     auto ch = r.h.find("connection");
     const bool keep = (ch == r.h.end() || lower(ch->second) != "close") && r.version == "HTTP/1.1";
     if (!try_native(t, c, r, keep)) hand_to_python(t, c, r, keep);
   }
+  return true;
 }
 
 void on_done(IoThread& t, Done& d) {
@@ -667,7 +678,7 @@ void on_readable(IoThread& t, Conn* c) {
     if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
     // EOF or error: what was complete is still answered (the Python
     // server reads requests until the stream ends), then the connection closes
-    if (!c->busy) process(t, c);
+    if (!c->busy && !process(t, c)) return;
     if (c->fd >= 0) {
       if (c->busy) {
         c->close_after = true;   // answer the request in flight, then close
