@@ -147,7 +147,7 @@ def parse_args(argv=None):
                         "exceeds the 256 MB Infinity Cache)")
     p.add_argument("--host-rows", type=int, default=8_000_000,
                    help="rows of the host-to-host (PCIe-inclusive) C2 leg (0 = skip)")
-    p.add_argument("--c5-http-qps", default="20000,60000,100000",
+    p.add_argument("--c5-http-qps", default="20000,100000,200000",
                    help="C5 over HTTP: offered req/s of the points (empty: skip); rank 0, "
                         "after the GPU legs, a server of one worker per GPU")
     p.add_argument("--c5-http-seconds", type=float, default=4.0)
@@ -655,9 +655,9 @@ def c5_http_leg(args, world):
     one worker process per GPU of the job (worker i drives GPU i), 4,096
     keep-alive connections from the C load generator (scripts/loadgen.c:
     open-loop Poisson arrivals of U{1..64}-row v1 :predict bodies, latency
-    from the scheduled arrival; 4 threads, each its own epoll loop).  Run on
-    rank 0 after every rank's GPU legs; the offered rates are totals for the
-    node, not per GPU."""
+    from the scheduled arrival; 4 threads, each its own epoll loop), 16 IO
+    threads over the workers.  Run on rank 0 after every rank's GPU legs; the
+    offered rates are totals for the node, not per GPU."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import bench_serving as bs
@@ -668,7 +668,7 @@ def c5_http_leg(args, world):
               "MASTER_PORT", "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
     qps = [float(q) for q in args.c5_http_qps.split(",") if q.strip()]
-    io = max(2, 8 // world)
+    io = max(2, 16 // world)
     try:
         pts = bs.serve_and_measure(qps, workers=world, io_threads=io,
                                    duration=args.c5_http_seconds, warmup=1.5, conns=4096,
