@@ -132,7 +132,8 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
                                   "--warmup", str(warmup), "--bodies", bodies,
                                   "--threads", str(loadgen_threads),
                                   "--path", "/v1/models/model:predict"],
-                                 capture_output=True, text=True, timeout=duration * 3 + 120)
+                                 capture_output=True, text=True,
+                                 timeout=duration + warmup + 60)   # loadgen drains by +30 s
             if out.returncode != 0:
                 raise RuntimeError(f"loadgen failed: {out.stderr[-2000:]}")
             res = json.loads(out.stdout)
