@@ -71,15 +71,19 @@ int kh_create(const kh_config* cfg, void** out);
  * out_elem_bytes (4: float32, 8: float64) each), converting each request's
  * float64 rows with kb_submit_convert's `transform` (low 8 bits; KH_CHECK_*
  * flags above them).  The server takes the
- * batcher's done callback (kb_set_done_callback).  -1 if the model already
- * has a route. */
+ * batcher's done callback (kb_set_done_callback).  n_labels > 0: the
+ * predictions are class indices (out_width 1), each answered with its label,
+ * labels[label_offsets[i] .. label_offsets[i + 1]) being label i rendered as
+ * json.dumps renders it (sklearnserver classifiers: classes_.take(index)).
+ * -1 if the model already has a route. */
 #define KH_CHECK_F32_FINITE (1 << 8)  /* hand to the application a body with a value
                                          that is +-inf after the float32 cast
                                          (sklearn's check_array on X.astype(float32)) */
 #define KH_CHECK_NO_NAN     (1 << 9)  /* ... or holding a NaN (estimators without
                                          missing-value support)                     */
 int kh_add_v1_predict(void* srv, const char* model, void* batcher, int32_t n_cols,
-                      int32_t out_width, int32_t out_elem_bytes, int32_t transform);
+                      int32_t out_width, int32_t out_elem_bytes, int32_t transform,
+                      const char* labels, const int32_t* label_offsets, int32_t n_labels);
 
 /* Stop answering the model natively (its requests go to the application):
  * the batcher's forming batch is flushed, the requests already submitted are

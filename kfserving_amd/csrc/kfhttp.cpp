@@ -58,6 +58,9 @@ struct Route {
   void* batcher = nullptr;
   RouteCtx* ctx = nullptr;
   int n_cols = 0, out_width = 0, out_elem = 0, transform = 0;
+  // class labels (kh_set_route_labels): the prediction is an index into them,
+  // each already rendered as json.dumps renders it
+  std::shared_ptr<const std::vector<std::string>> labels;
 };
 
 struct Conn {
@@ -588,7 +591,11 @@ void answer_native(Conn* c, const kb_completion& d, const std::string& err) {
         } else {
           std::memcpy(&v, c->res.data() + at * 8, 8);
         }
-        append_double(body, v);
+        const auto* lab = c->route.labels.get();
+        if (lab && v >= 0 && v < static_cast<double>(lab->size()))
+          body += (*lab)[static_cast<size_t>(v)];   // classes_.take(index)
+        else
+          append_double(body, v);
       }
       if (w > 1) body += ']';
     }
@@ -852,9 +859,11 @@ int kh_create(const kh_config* cfg, void** out) {
 }
 
 int kh_add_v1_predict(void* h, const char* model, void* batcher, int32_t n_cols,
-                      int32_t out_width, int32_t out_elem_bytes, int32_t transform) {
+                      int32_t out_width, int32_t out_elem_bytes, int32_t transform,
+                      const char* labels, const int32_t* label_offsets, int32_t n_labels) {
   if (!h || !model || !batcher || n_cols <= 0 || out_width <= 0 ||
-      (out_elem_bytes != 4 && out_elem_bytes != 8))
+      (out_elem_bytes != 4 && out_elem_bytes != 8) || n_labels < 0 ||
+      (n_labels > 0 && (!labels || !label_offsets || out_width != 1)))
     return -1;
   Server& s = *static_cast<Server*>(h);
   RouteCtx* ctx;
@@ -874,6 +883,13 @@ int kh_add_v1_predict(void* h, const char* model, void* batcher, int32_t n_cols,
   r.out_width = out_width;
   r.out_elem = out_elem_bytes;
   r.transform = transform;
+  if (n_labels > 0) {
+    auto v = std::make_shared<std::vector<std::string>>();
+    for (int32_t i = 0; i < n_labels; ++i)
+      v->emplace_back(labels + label_offsets[i],
+                      static_cast<size_t>(label_offsets[i + 1] - label_offsets[i]));
+    r.labels = v;
+  }
   std::lock_guard<std::mutex> lk(s.rmu);
   s.routes[model] = r;
   return 0;

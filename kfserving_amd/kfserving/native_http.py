@@ -66,7 +66,8 @@ def load_library() -> ctypes.CDLL:
     lib.kh_create.restype = ctypes.c_int
     lib.kh_create.argtypes = [ctypes.POINTER(KhConfig), ctypes.POINTER(vp)]
     lib.kh_add_v1_predict.restype = ctypes.c_int
-    lib.kh_add_v1_predict.argtypes = [vp, ctypes.c_char_p, vp, i32, i32, i32, i32]
+    lib.kh_add_v1_predict.argtypes = [vp, ctypes.c_char_p, vp, i32, i32, i32, i32,
+                                      ctypes.c_char_p, ctypes.POINTER(i32), i32]
     lib.kh_remove_route.restype = ctypes.c_int
     lib.kh_remove_route.argtypes = [vp, ctypes.c_char_p]
     lib.kh_start.restype = ctypes.c_int
@@ -129,8 +130,10 @@ def _spec_of(batcher, model):
         return None
     f = model._forest
     import numpy as np
+    labels = getattr(model, "native_v1_labels", None)
     return (batcher._nb._h, f.n_features, f.output_width(OUT_PREDICT),
-            np.dtype(f.output_dtype(OUT_PREDICT)).itemsize, int(model.native_v1_transform))
+            np.dtype(f.output_dtype(OUT_PREDICT)).itemsize, int(model.native_v1_transform),
+            labels() if callable(labels) else None)
 
 
 class NativeFrontEnd:
@@ -163,10 +166,19 @@ class NativeFrontEnd:
         self._register(name, spec)
 
     def _register(self, name, spec) -> None:
-        h, F, w, e, tr = spec
+        h, F, w, e, tr, labels = spec
         if name in self.routes:
             self._lib.kh_remove_route(self._h, name.encode())
-        if self._lib.kh_add_v1_predict(self._h, name.encode(), h, F, w, e, tr) == 0:
+            del self.routes[name]
+        blob, arr, n = None, None, 0
+        if labels is not None:
+            offs = [0]
+            for lab in labels:
+                offs.append(offs[-1] + len(lab.encode()))
+            blob = "".join(labels).encode()
+            arr = (ctypes.c_int32 * len(offs))(*offs)
+            n = len(labels)
+        if self._lib.kh_add_v1_predict(self._h, name.encode(), h, F, w, e, tr, blob, arr, n) == 0:
             self.routes[name] = h
 
     def _on_batcher(self, event: str, name: str, kind: str, batcher) -> None:

@@ -86,13 +86,21 @@ class SKLearnModel(GPUForestMixin, KFModel):  # pylint:disable=c-extension-no-me
     @property
     def native_v1_transform(self):
         """The native HTTP route's element rule and checks (kfhttp.h): the
-        float32 cast, a value that overflows it or a NaN the estimator
-        rejects sends the request to predict's own checks; classifiers (label
-        mapping) keep the application's path."""
+        float32 cast; a value that overflows it, or a NaN the estimator
+        rejects, sends the request to predict's own checks."""
         f = self._forest
-        if f is None or f.meta.get("classes") is not None:
+        if f is None:
             return None
         return (1 << 8) | (0 if f.meta.get("allow_nan", True) else (1 << 9))
+
+    def native_v1_labels(self):
+        """A classifier's labels as its predict renders them
+        (classes.take(index).tolist() -> json.dumps), for the native route."""
+        import json
+        classes = self._forest.meta.get("classes")
+        if classes is None:
+            return None
+        return [json.dumps(c) for c in np.asarray(classes).tolist()]
 
     def native_rows(self, chunk, kind: str) -> np.ndarray:
         # the same checks for V2 tensors and instances (predict_tensor)

@@ -319,3 +319,42 @@ def test_sklearn_regressor_route_and_its_checks(golden, tmp_path):
         finally:
             nat.stop()
             py.stop()
+
+
+def test_sklearn_classifier_route_answers_labels(golden, tmp_path):
+    """A classifier's native route answers class labels, rendered as its
+    predict renders classes.take(index).tolist() (numeric and string
+    labels), byte for byte as the asyncio server."""
+    from kfserving_amd.sklearnserver import SKLearnModel
+    g = np.load(os.path.join(golden, "sk_rf_clf.npz"))
+    X = np.nan_to_num(g["X"][:8]).astype(np.float64)
+    for labels in (None, np.array(["setosa", "versiécolor", 'vir"ginica', "x", "y"])):
+        runs = []
+        for native in (True, False):
+            d = tmp_path / f"{labels is None}{native}"
+            d.mkdir(parents=True)
+            shutil.copy(os.path.join(golden, "sk_rf_clf_model.npz"), str(d / "model.npz"))
+            m = SKLearnModel("clf", str(d))
+            assert m.load()
+            if labels is not None:
+                k = len(m._forest.meta["classes"])
+                m._forest.meta["classes"] = labels[:k]
+            m.predict_matrix = (lambda mm: lambda X, kind=OUT_PREDICT:
+                                canon_eval.predict(mm._forest, X, kind))(m)
+            srv = KFServer(max_batchsize=64, max_latency_ms=3)
+            srv.native_http = native
+            srv.register_model(m)
+            runs.append(_Running(srv))
+        nat, py = runs
+        _wait_front_end(nat)
+        try:
+            assert "clf" in nat.server.front_end.routes
+            for k in (1, 3, 8):
+                body = json.dumps({"instances": X[:k].tolist()}).encode()
+                a = nat.fetch("/v1/models/clf:predict", "POST", body)
+                b = py.fetch("/v1/models/clf:predict", "POST", body)
+                assert a[0] == b[0] == 200 and _norm(a[2]) == _norm(b[2]), (a[2], b[2])
+            assert nat.server.front_end.stats()["native_requests"] >= 3
+        finally:
+            nat.stop()
+            py.stop()
