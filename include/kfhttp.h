@@ -85,6 +85,15 @@ int kh_add_v1_predict(void* srv, const char* model, void* batcher, int32_t n_col
                       int32_t out_width, int32_t out_elem_bytes, int32_t transform,
                       const char* labels, const int32_t* label_offsets, int32_t n_labels);
 
+/* kh_add_v1_predict for an lgbserver model: bodies are {"inputs": [{"<column>":
+ * [...], ...}, ...]} (lgbserver/model.py:44-54), read into float64 rows by
+ * kf_parse_inputs with the model's n_cols feature names (name j at
+ * names[name_offsets[j] .. name_offsets[j + 1])); a body outside its subset
+ * goes to the application.  Rows are copied as they are (KB_IN_PLAIN). */
+int kh_add_v1_inputs_predict(void* srv, const char* model, void* batcher, int32_t n_cols,
+                             int32_t out_width, int32_t out_elem_bytes, const char* names,
+                             const int32_t* name_offsets);
+
 /* Stop answering the model natively (its requests go to the application):
  * the batcher's forming batch is flushed, the requests already submitted are
  * answered, and the batcher's done callback is detached before this returns,

@@ -50,6 +50,24 @@ int kf_parse_instances(const char* body, int64_t len, double* out, int64_t cap,
 int kf_parse_instances_mt(const char* body, int64_t len, double* out, int64_t cap,
                           int64_t* rows, int64_t* cols, int32_t threads);
 
+/* A v1 lgbserver body {"inputs": [{"<column>": [v, ...], ...}, ...]} as the
+ * float64 [rows, n_names] matrix lgbserver builds from it
+ * (python/lgbserver/lgbserver/model.py:46-50: pd.DataFrame(i,
+ * columns=booster.feature_name()) per element, concatenated): columns taken
+ * by name in the model's order, an absent column NaN, keys the model does not
+ * name skipped, a column of numbers with nulls beside them read with null as
+ * NaN, a column of booleans as 1 / 0.  Anything pandas and lightgbm would
+ * treat otherwise -- booleans mixed with numbers or nulls, an all-null
+ * column, strings, nested values in a named column, duplicate or escaped
+ * keys, columns of unequal length, no rows at all -- returns KF_FALLBACK
+ * (kfserving_amd.tree_model.lgb_matrix_from_inputs then decides, as the
+ * reference does).  names: the feature names back to back, name j at
+ * names[name_offsets[j] .. name_offsets[j + 1]).  KF_ERR_SPACE: out holds
+ * fewer than *rows * n_names values. */
+int kf_parse_inputs(const char* body, int64_t len, const char* names,
+                    const int32_t* name_offsets, int32_t n_names, double* out, int64_t cap,
+                    int64_t* rows);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -58,9 +58,13 @@ struct Route {
   void* batcher = nullptr;
   RouteCtx* ctx = nullptr;
   int n_cols = 0, out_width = 0, out_elem = 0, transform = 0;
-  // class labels (kh_set_route_labels): the prediction is an index into them,
+  // class labels (kh_add_v1_predict): the prediction is an index into them,
   // each already rendered as json.dumps renders it
   std::shared_ptr<const std::vector<std::string>> labels;
+  // lgbserver routes (kh_add_v1_inputs_predict): bodies are {"inputs": ...},
+  // columns by these names (back to back, offsets n_cols + 1)
+  std::shared_ptr<const std::string> names;
+  std::shared_ptr<const std::vector<int32_t>> name_offsets;
 };
 
 struct Conn {
@@ -539,10 +543,24 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   const size_t cap = (r.body.size() + 1) / 2;
   if (xb.size() < cap) xb.resize(cap);
   int64_t rows = 0, cols = 0;
-  if (kf_parse_instances(r.body.data(), static_cast<int64_t>(r.body.size()), xb.data(),
-                         static_cast<int64_t>(xb.size()), &rows, &cols) != KF_PARSED ||
-      rows <= 0 || cols != route.n_cols)
+  if (route.names) {   // lgbserver: {"inputs": [{column: [...]}, ...]}
+    const int32_t* offs = route.name_offsets->data();
+    int rc = kf_parse_inputs(r.body.data(), static_cast<int64_t>(r.body.size()),
+                             route.names->data(), offs, route.n_cols, xb.data(),
+                             static_cast<int64_t>(xb.size()), &rows);
+    if (rc == KF_ERR_SPACE && rows > 0 && rows <= (int64_t(1) << 24)) {   // absent columns
+      xb.resize(static_cast<size_t>(rows) * route.n_cols);               // are NaN: more
+      rc = kf_parse_inputs(r.body.data(), static_cast<int64_t>(r.body.size()),   // values
+                           route.names->data(), offs, route.n_cols, xb.data(),   // than text
+                           static_cast<int64_t>(xb.size()), &rows);
+    }
+    if (rc != KF_PARSED || rows <= 0) return false;
+    cols = route.n_cols;
+  } else if (kf_parse_instances(r.body.data(), static_cast<int64_t>(r.body.size()), xb.data(),
+                                static_cast<int64_t>(xb.size()), &rows, &cols) != KF_PARSED ||
+             rows <= 0 || cols != route.n_cols) {
     return false;
+  }
   if (route.transform & (KH_CHECK_F32_FINITE | KH_CHECK_NO_NAN)) {
     const bool fin = route.transform & KH_CHECK_F32_FINITE, nonan = route.transform & KH_CHECK_NO_NAN;
     for (int64_t i = 0; i < rows * cols; ++i) {
@@ -858,9 +876,10 @@ int kh_create(const kh_config* cfg, void** out) {
   return 0;
 }
 
-int kh_add_v1_predict(void* h, const char* model, void* batcher, int32_t n_cols,
-                      int32_t out_width, int32_t out_elem_bytes, int32_t transform,
-                      const char* labels, const int32_t* label_offsets, int32_t n_labels) {
+static int add_route(void* h, const char* model, void* batcher, int32_t n_cols,
+                     int32_t out_width, int32_t out_elem_bytes, int32_t transform,
+                     const char* labels, const int32_t* label_offsets, int32_t n_labels,
+                     const char* names, const int32_t* name_offsets) {
   if (!h || !model || !batcher || n_cols <= 0 || out_width <= 0 ||
       (out_elem_bytes != 4 && out_elem_bytes != 8) || n_labels < 0 ||
       (n_labels > 0 && (!labels || !label_offsets || out_width != 1)))
@@ -890,9 +909,29 @@ int kh_add_v1_predict(void* h, const char* model, void* batcher, int32_t n_cols,
                       static_cast<size_t>(label_offsets[i + 1] - label_offsets[i]));
     r.labels = v;
   }
+  if (names) {   // an lgbserver route: column names, in the model's order
+    r.names = std::make_shared<const std::string>(names, static_cast<size_t>(name_offsets[n_cols]));
+    r.name_offsets = std::make_shared<const std::vector<int32_t>>(name_offsets,
+                                                                  name_offsets + n_cols + 1);
+  }
   std::lock_guard<std::mutex> lk(s.rmu);
   s.routes[model] = r;
   return 0;
+}
+
+int kh_add_v1_predict(void* h, const char* model, void* batcher, int32_t n_cols,
+                      int32_t out_width, int32_t out_elem_bytes, int32_t transform,
+                      const char* labels, const int32_t* label_offsets, int32_t n_labels) {
+  return add_route(h, model, batcher, n_cols, out_width, out_elem_bytes, transform, labels,
+                   label_offsets, n_labels, nullptr, nullptr);
+}
+
+int kh_add_v1_inputs_predict(void* h, const char* model, void* batcher, int32_t n_cols,
+                             int32_t out_width, int32_t out_elem_bytes, const char* names,
+                             const int32_t* name_offsets) {
+  if (!names || !name_offsets) return -1;
+  return add_route(h, model, batcher, n_cols, out_width, out_elem_bytes, KB_IN_PLAIN, nullptr,
+                   nullptr, 0, names, name_offsets);
 }
 
 int kh_remove_route(void* h, const char* model) {

@@ -446,3 +446,168 @@ extern "C" int kf_parse_instances_mt(const char* body, int64_t len, double* out,
   *cols = c;
   return KF_PARSED;
 }
+
+// ------------------------------------------------------ lgbserver "inputs"
+namespace {
+
+// skip one JSON value of any kind at sc.p (a key the model does not read)
+bool skip_value(Scanner& sc, int depth) {
+  if (depth > 64) return false;
+  sc.ws();
+  if (sc.p >= sc.end) return false;
+  const char c = *sc.p;
+  if (c == '"') {
+    ++sc.p;
+    while (sc.p < sc.end && *sc.p != '"') {
+      if (*sc.p == '\\') ++sc.p;
+      ++sc.p;
+    }
+    return sc.eat('"');
+  }
+  if (c == '{' || c == '[') {
+    const char close = c == '{' ? '}' : ']';
+    ++sc.p;
+    sc.ws();
+    if (sc.eat(close)) return true;
+    for (;;) {
+      if (c == '{') {
+        sc.ws();
+        if (!skip_value(sc, depth + 1)) return false;   // the key
+        sc.ws();
+        if (!sc.eat(':')) return false;
+      }
+      if (!skip_value(sc, depth + 1)) return false;
+      sc.ws();
+      if (sc.eat(',')) continue;
+      return sc.eat(close);
+    }
+  }
+  if (sc.lit("true", 4) || sc.lit("false", 5) || sc.lit("null", 4)) return true;
+  double v;
+  return sc.number(&v);
+}
+
+}  // namespace
+
+extern "C" int kf_parse_inputs(const char* body, int64_t len, const char* names,
+                               const int32_t* name_offsets, int32_t n_names, double* out,
+                               int64_t cap, int64_t* rows) {
+  if (!body || len < 0 || !rows || n_names <= 0 || !names || !name_offsets) return KF_FALLBACK;
+  *rows = 0;
+  // the feature names, by text
+  std::vector<std::pair<const char*, size_t>> nm(static_cast<size_t>(n_names));
+  for (int32_t j = 0; j < n_names; ++j)
+    nm[static_cast<size_t>(j)] = {names + name_offsets[j],
+                                  static_cast<size_t>(name_offsets[j + 1] - name_offsets[j])};
+  auto find = [&](const char* k, size_t n) -> int {
+    for (int32_t j = 0; j < n_names; ++j)
+      if (nm[static_cast<size_t>(j)].second == n &&
+          std::memcmp(nm[static_cast<size_t>(j)].first, k, n) == 0)
+        return j;
+    return -1;
+  };
+  Scanner sc{body, body + len};
+  sc.ws();
+  if (!sc.eat('{')) return KF_FALLBACK;
+  sc.ws();
+  if (!sc.lit("\"inputs\"", 8)) return KF_FALLBACK;
+  sc.ws();
+  if (!sc.eat(':')) return KF_FALLBACK;
+  sc.ws();
+  if (!sc.eat('[')) return KF_FALLBACK;
+  sc.ws();
+  if (sc.p < sc.end && *sc.p == ']') return KF_FALLBACK;   // no inputs: the error path
+  int64_t R = 0;
+  bool overflow = false;
+  std::vector<std::vector<double>> col(static_cast<size_t>(n_names));
+  std::vector<char> seen(static_cast<size_t>(n_names));
+  for (;;) {   // one element of "inputs": an object of columns
+    sc.ws();
+    if (!sc.eat('{')) return KF_FALLBACK;
+    std::fill(seen.begin(), seen.end(), 0);
+    for (auto& v : col) v.clear();
+    int64_t n = -1;   // this element's rows
+    sc.ws();
+    if (!sc.eat('}')) {
+      for (;;) {
+        sc.ws();
+        if (!sc.eat('"')) return KF_FALLBACK;
+        const char* k = sc.p;
+        while (sc.p < sc.end && *sc.p != '"' && *sc.p != '\\') ++sc.p;
+        if (sc.p >= sc.end || *sc.p == '\\') return KF_FALLBACK;   // escapes: json.loads
+        const size_t kn = static_cast<size_t>(sc.p - k);
+        ++sc.p;
+        sc.ws();
+        if (!sc.eat(':')) return KF_FALLBACK;
+        sc.ws();
+        const int j = find(k, kn);
+        if (j < 0) {
+          if (!skip_value(sc, 0)) return KF_FALLBACK;   // a key the model drops
+        } else {
+          if (seen[static_cast<size_t>(j)]) return KF_FALLBACK;   // duplicate: the last wins
+          seen[static_cast<size_t>(j)] = 1;
+          // a column: numbers with None beside them (None -> NaN), or all
+          // booleans; anything else is pandas' (tree_model._numeric_column)
+          if (!sc.eat('[')) return KF_FALLBACK;
+          std::vector<double>& v = col[static_cast<size_t>(j)];
+          int n_num = 0, n_bool = 0, n_none = 0;
+          sc.ws();
+          if (!sc.eat(']')) {
+            for (;;) {
+              sc.ws();
+              double x;
+              if (sc.lit("null", 4)) {
+                ++n_none;
+                x = std::nan("");
+              } else if (sc.lit("true", 4)) {
+                ++n_bool;
+                x = 1.0;
+              } else if (sc.lit("false", 5)) {
+                ++n_bool;
+                x = 0.0;
+              } else if (sc.number(&x)) {
+                ++n_num;
+              } else {
+                return KF_FALLBACK;
+              }
+              v.push_back(x);
+              sc.ws();
+              if (sc.eat(',')) continue;
+              if (sc.eat(']')) break;
+              return KF_FALLBACK;
+            }
+          }
+          if (n_bool ? (n_num || n_none) : (n_num == 0 && !v.empty())) return KF_FALLBACK;
+          const int64_t m = static_cast<int64_t>(v.size());
+          if (n >= 0 && m != n) return KF_FALLBACK;   // columns of unequal length
+          n = m;
+        }
+        sc.ws();
+        if (sc.eat(',')) continue;
+        if (sc.eat('}')) break;
+        return KF_FALLBACK;
+      }
+    }
+    if (n < 0) n = 0;
+    for (int64_t r = 0; r < n; ++r)
+      for (int32_t j = 0; j < n_names; ++j) {
+        const int64_t at = (R + r) * n_names + j;
+        const double x = seen[static_cast<size_t>(j)] ? col[static_cast<size_t>(j)][static_cast<size_t>(r)]
+                                                      : std::nan("");
+        if (at < cap) out[at] = x;
+        else overflow = true;
+      }
+    R += n;
+    sc.ws();
+    if (sc.eat(',')) continue;
+    if (sc.eat(']')) break;
+    return KF_FALLBACK;
+  }
+  sc.ws();
+  if (!sc.eat('}')) return KF_FALLBACK;
+  sc.ws();
+  if (sc.p != sc.end) return KF_FALLBACK;
+  if (R == 0) return KF_FALLBACK;   // no rows: lgbserver's error
+  *rows = R;
+  return overflow ? KF_ERR_SPACE : KF_PARSED;
+}

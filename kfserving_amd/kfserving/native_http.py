@@ -25,7 +25,8 @@ from .kfmodel import KFModel
 
 KH_ABI_VERSION = 1
 
-EXPORTED_SYMBOLS = ("kh_create", "kh_add_v1_predict", "kh_remove_route", "kh_start",
+EXPORTED_SYMBOLS = ("kh_create", "kh_add_v1_predict", "kh_add_v1_inputs_predict",
+                    "kh_remove_route", "kh_start",
                     "kh_fallback_fd", "kh_next_fallback", "kh_respond", "kh_get_stats",
                     "kh_destroy", "kh_repr_double", "kh_abi_version")
 
@@ -68,6 +69,9 @@ def load_library() -> ctypes.CDLL:
     lib.kh_add_v1_predict.restype = ctypes.c_int
     lib.kh_add_v1_predict.argtypes = [vp, ctypes.c_char_p, vp, i32, i32, i32, i32,
                                       ctypes.c_char_p, ctypes.POINTER(i32), i32]
+    lib.kh_add_v1_inputs_predict.restype = ctypes.c_int
+    lib.kh_add_v1_inputs_predict.argtypes = [vp, ctypes.c_char_p, vp, i32, i32, i32,
+                                             ctypes.c_char_p, ctypes.POINTER(i32)]
     lib.kh_remove_route.restype = ctypes.c_int
     lib.kh_remove_route.argtypes = [vp, ctypes.c_char_p]
     lib.kh_start.restype = ctypes.c_int
@@ -116,11 +120,24 @@ def route_spec(app, model, name: str):
             type(model).postprocess is not KFModel.postprocess:
         return None
     try:
-        batcher = app._batcher_for(model, name, "instances")
+        batcher = app._batcher_for(model, name, route_kind(model))
     except Exception as e:   # no device here: the application's path serves it
         logging.warning("no native route for %s: %s", name, e)
         return None
     return _spec_of(batcher, model)
+
+
+def route_kind(model) -> str:
+    """The batcher kind the route's requests take in the application:
+    lgbserver's ``inputs`` bodies, everyone else's ``instances``."""
+    return "inputs" if getattr(model, "native_v1_names", None) is not None else "instances"
+
+
+def _blob(strings):
+    offs = [0]
+    for x in strings:
+        offs.append(offs[-1] + len(x.encode()))
+    return "".join(strings).encode(), (ctypes.c_int32 * len(offs))(*offs)
 
 
 def _spec_of(batcher, model):
@@ -131,9 +148,10 @@ def _spec_of(batcher, model):
     f = model._forest
     import numpy as np
     labels = getattr(model, "native_v1_labels", None)
+    names = getattr(model, "native_v1_names", None)
     return (batcher._nb._h, f.n_features, f.output_width(OUT_PREDICT),
             np.dtype(f.output_dtype(OUT_PREDICT)).itemsize, int(model.native_v1_transform),
-            labels() if callable(labels) else None)
+            labels() if callable(labels) else None, names() if callable(names) else None)
 
 
 class NativeFrontEnd:
@@ -166,23 +184,27 @@ class NativeFrontEnd:
         self._register(name, spec)
 
     def _register(self, name, spec) -> None:
-        h, F, w, e, tr, labels = spec
+        h, F, w, e, tr, labels, names = spec
         if name in self.routes:
             self._lib.kh_remove_route(self._h, name.encode())
             del self.routes[name]
-        blob, arr, n = None, None, 0
-        if labels is not None:
-            offs = [0]
-            for lab in labels:
-                offs.append(offs[-1] + len(lab.encode()))
-            blob = "".join(labels).encode()
-            arr = (ctypes.c_int32 * len(offs))(*offs)
-            n = len(labels)
-        if self._lib.kh_add_v1_predict(self._h, name.encode(), h, F, w, e, tr, blob, arr, n) == 0:
+        if names is not None:
+            blob, offs = _blob(names)
+            rc = self._lib.kh_add_v1_inputs_predict(self._h, name.encode(), h, F, w, e, blob, offs)
+        else:
+            blob, offs, n = None, None, 0
+            if labels is not None:
+                blob, offs = _blob(labels)
+                n = len(labels)
+            rc = self._lib.kh_add_v1_predict(self._h, name.encode(), h, F, w, e, tr, blob, offs, n)
+        if rc == 0:
             self.routes[name] = h
 
     def _on_batcher(self, event: str, name: str, kind: str, batcher) -> None:
-        if kind != "instances" or self._h is None:
+        if kind not in ("instances", "inputs") or self._h is None:
+            return
+        model = batcher.model
+        if kind != route_kind(model):
             return
         if event == "retire" and name in self.routes:
             # detach before the batcher stops: kh_remove_route returns once the
@@ -190,7 +212,6 @@ class NativeFrontEnd:
             self._lib.kh_remove_route(self._h, name.encode())
             del self.routes[name]
         elif event == "create":
-            model = batcher.model
             if route_spec_static(self.app, model) and not self.routes.get(name):
                 spec = _spec_of(batcher, model)
                 if spec is not None:

@@ -59,6 +59,14 @@ class LightGBMModel(GPUForestMixin, KFModel):
         except Exception as e:
             raise Exception("Failed to predict %s" % e)
 
+    # the native HTTP front end (kfhttp.h) reads batched v1 {"inputs": ...}
+    # bodies of this model itself (kf_parse_inputs: columns by these names, the
+    # subset lgb_matrix_from_inputs takes without pandas), rows as they are
+    native_v1_transform = 0
+
+    def native_v1_names(self):
+        return self.feature_name()
+
     # KFServer's in-process batcher (kfserving_amd.batcher.ModelBatcher, kind
     # "inputs"): one request's rows as the float64 matrix its columns select,
     # then one predict over the concatenated rows of a batch

@@ -358,3 +358,56 @@ def test_sklearn_classifier_route_answers_labels(golden, tmp_path):
         finally:
             nat.stop()
             py.stop()
+
+
+def test_lgbserver_inputs_route_bytes_equal_python_server(golden, tmp_path):
+    """lgbserver's {"inputs": [...]} bodies on the native route
+    (kf_parse_inputs): columns by name, absent columns NaN, dropped keys of
+    any shape, nulls, boolean columns -- and every body outside that subset
+    (booleans mixed with numbers, all-null or string columns, duplicate or
+    escaped keys, unequal columns, no rows, non-object elements) answered by
+    the application; bytes identical to the asyncio server."""
+    from tests.test_lgb_batching import _lgb_model
+    runs = []
+    for native in (True, False):
+        srv = KFServer(max_batchsize=64, max_latency_ms=3)
+        srv.native_http = native
+        (tmp_path / ("n" if native else "p")).mkdir()
+        srv.register_model(_lgb_model(golden, tmp_path / ("n" if native else "p")))
+        runs.append(_Running(srv))
+    nat, py = runs
+    _wait_front_end(nat)
+    names = ["sepal_length_(cm)", "sepal_width_(cm)", "petal_length_(cm)", "petal_width_(cm)"]
+    a, b, c, d = names
+    bodies = [
+        {"inputs": [{a: [5.1, 6.2], b: [3.5, 2.9], c: [1.4, 4.3], d: [0.2, 1.3]}]},
+        {"inputs": [{d: [1.8], c: [5.0], a: [6.3], b: [2.5], "x": [1, 2, 3]}]},
+        {"inputs": [{a: [5.0, 5.5], c: [1.0, None]}, {b: [3.0], d: [0.1]}]},
+        {"inputs": [{a: [True, False], b: [1, 2], c: [0, 0], d: [2, 3],
+                     "meta": {"k": ["s", {"n": None}], "t": True}}]},
+        {"inputs": [{a: [1e-320, -0.0], b: [1e300, 3], c: [float("nan"), 2], d: [4, 5]}]},
+        {"inputs": [{a: [True, 1.0], b: [1.0, 2.0]}]},            # bool mixed: pandas
+        {"inputs": [{a: [None, None], b: [1.0, 2.0]}]},           # all-null column
+        {"inputs": [{a: ["1.0"], b: [1.0]}]},                     # strings
+        {"inputs": [{a: [1.0, 2.0], b: [1.0]}]},                  # unequal lengths
+        {"inputs": [{"x": [1.0]}]},                               # no rows
+        {"inputs": []},
+        {"inputs": [3]},
+        {"inputs": 3},
+    ]
+    raw = [
+        b'{"inputs": [{"sepal_length_(cm)": [1.0], "sepal_length_(cm)": [2.0]}]}',
+        b'{"inputs": [{"sepal_length_\\u0028cm)": [1.0]}]}',
+        b'{"inputs": [{"sepal_length_(cm)": [12345678901234567890123], "sepal_width_(cm)": [1]}]}',
+    ]
+    try:
+        assert "lightgbm" in nat.server.front_end.routes
+        for body in [json.dumps(x).encode() for x in bodies] + raw:
+            x = nat.fetch("/v1/models/lightgbm:predict", "POST", body)
+            y = py.fetch("/v1/models/lightgbm:predict", "POST", body)
+            assert x[0] == y[0] and x[1] == y[1] and _norm(x[2]) == _norm(y[2]), (body, x, y)
+        st = nat.server.front_end.stats()
+        assert st["native_requests"] >= 5 and st["python_requests"] >= 8
+    finally:
+        nat.stop()
+        py.stop()
