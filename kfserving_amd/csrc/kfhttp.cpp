@@ -476,14 +476,25 @@ Parse parse_request(const std::string& in, size_t start, int64_t max_body, Req* 
   return Parse::kDone;
 }
 
-// "/v1/models/<name>:predict" (query string dropped): the model name, or ""
-std::string predict_route(const std::string& target) {
+// "/v1/models/<name>:predict" or "/v2/models/<name>/infer" (query string
+// dropped): the model name, or ""; *v2 tells which
+std::string predict_route(const std::string& target, bool* v2) {
   const std::string path = target.substr(0, target.find('?'));
-  static const std::string pre = "/v1/models/", suf = ":predict";
-  if (path.size() <= pre.size() + suf.size() || path.compare(0, pre.size(), pre) != 0 ||
-      path.compare(path.size() - suf.size(), suf.size(), suf) != 0)
+  static const std::string pre1 = "/v1/models/", suf1 = ":predict";
+  static const std::string pre2 = "/v2/models/", suf2 = "/infer";
+  auto match = [&path](const std::string& pre, const std::string& suf) {
+    return path.size() > pre.size() + suf.size() && path.compare(0, pre.size(), pre) == 0 &&
+           path.compare(path.size() - suf.size(), suf.size(), suf) == 0;
+  };
+  size_t a, b;
+  if (match(pre1, suf1)) {
+    a = pre1.size(), b = suf1.size(), *v2 = false;
+  } else if (match(pre2, suf2)) {
+    a = pre2.size(), b = suf2.size(), *v2 = true;
+  } else {
     return std::string();
-  std::string name = path.substr(pre.size(), path.size() - pre.size() - suf.size());
+  }
+  std::string name = path.substr(a, path.size() - a - b);
   for (char ch : name)
     if (!(std::isalnum(static_cast<unsigned char>(ch)) || ch == '_' || ch == '-')) return std::string();
   return name;
@@ -514,10 +525,17 @@ void hand_to_python(IoThread& t, Conn* c, Req& r, bool keep) {
 bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   Server& s = *t.srv;
   if (r.method != "POST" || r.body.size() >= KF_MT_MIN_BYTES) return false;   // big bodies: the
-  const std::string name = predict_route(r.target);                          // threaded parser
+  bool v2 = false;                                                           // threaded parser
+  const std::string name = predict_route(r.target, &v2);
   if (name.empty()) return false;
   for (const char* h : {"ce-specversion", "ce-source", "ce-type", "ce-id"})
     if (r.h.count(h)) return false;   // binary CloudEvents: the application's path
+  // /v2/.../infer answers a v1 body as :predict does (ref kfserver.py:77-78);
+  // a V2 tensor request (a binary tail, or a "datatype" in the body) is the
+  // application's
+  if (v2 && (r.h.count("inference-header-content-length") ||
+             r.body.find("\"datatype\"") != std::string::npos))
+    return false;
   Route route;
   {
     // the reservation is taken under the route lock: kh_remove_route erases

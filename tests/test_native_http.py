@@ -127,8 +127,13 @@ def test_native_predict_bytes_equal_python_server(golden, tmp_path):
             assert {k: v for k, v in a[1].items()} == {k: v for k, v in b[1].items()}
             assert _norm(a[2]) == _norm(b[2])
             assert json.loads(a[2])["batchId"]
+            # /v2/.../infer answers a v1 body as :predict (ref kfserver.py:77-78)
+            a = nat.fetch("/v2/models/xgboost-iris/infer", "POST", body)
+            b = py.fetch("/v2/models/xgboost-iris/infer", "POST", body)
+            assert (a[0], dict(a[1].items())) == (b[0], dict(b[1].items()))
+            assert _norm(a[2]) == _norm(b[2])
         st = fe.stats()
-        assert st["native_requests"] >= 14 and st["python_requests"] == 0
+        assert st["native_requests"] >= 28 and st["python_requests"] == 0
     finally:
         nat.stop()
         py.stop()
@@ -153,6 +158,12 @@ def test_fallback_routes_and_errors_equal_python_server(golden, tmp_path):
         ("/v1/models/xgboost-iris:predict", "POST", b'{"instances": [[1, 2, 3, 4]]}',
          {"ce-specversion": "1.0", "ce-source": "s", "ce-type": "t", "ce-id": "1",
           "content-type": "application/json"}),
+        ("/v2/models/xgboost-iris/infer", "POST", b'{"instances": [[1, 2, 3, 4]]}',
+         {"Inference-Header-Content-Length": "29"}),
+        ("/v2/models/xgboost-iris/infer", "POST", b'{"instances": [[1, 2, 3, 4]]}',
+         {"Inference-Header-Content-Length": "12"}),
+        ("/v2/models/nope/infer", "POST", b'{"instances": [[1, 2, 3, 4]]}', {}),
+        ("/v2/models/xgboost-iris/infer", "GET", None, {}),
     ]
     try:
         for path, method, body, hdrs in cases:
