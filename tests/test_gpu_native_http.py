@@ -51,8 +51,10 @@ def test_native_http_c2_bytes_equal_python_server(tmp_path):
             X = rng.standard_normal((int(rng.integers(1, 65)), 28)).astype(np.float32)
             X[rng.random(X.shape) < 0.05] = 0.0          # DMatrix(list): missing
             body = json.dumps({"instances": X.tolist()}).encode()
-            a = nat.fetch("/v1/models/model:predict", "POST", body)
-            b = py.fetch("/v1/models/model:predict", "POST", body)
+            # every other body on /v2/.../infer, which takes a v1 body as :predict
+            path = "/v1/models/model:predict" if i % 2 == 0 else "/v2/models/model/infer"
+            a = nat.fetch(path, "POST", body)
+            b = py.fetch(path, "POST", body)
             assert a[0] == b[0] == 200 and a[1] == b[1]
             assert _norm(a[2]) == _norm(b[2])
             got = np.asarray(json.loads(a[2])["predictions"])
