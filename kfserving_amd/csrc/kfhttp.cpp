@@ -438,7 +438,10 @@ Parse parse_request(const std::string& in, size_t start, int64_t max_body, Req* 
   auto te = r->h.find("transfer-encoding");
   r->body.clear();
   if (te != r->h.end() && lower(te->second) == "chunked") {
+    // the chunks' spans first; the body is copied only once it is all here
+    // (a body arriving over many reads is re-parsed after each of them)
     int64_t total = 0;
+    std::vector<std::pair<size_t, size_t>> spans;
     for (;;) {
       k = take_line(in, pos, line);
       if (k == 0) return Parse::kIncomplete;
@@ -456,12 +459,14 @@ Parse parse_request(const std::string& in, size_t start, int64_t max_body, Req* 
       total += n;
       if (total > max_body) return Parse::kTooLarge;
       if (in.size() - pos < static_cast<size_t>(n)) return Parse::kIncomplete;
-      r->body.append(in, pos, static_cast<size_t>(n));
+      spans.emplace_back(pos, static_cast<size_t>(n));
       pos += static_cast<size_t>(n);
       k = take_line(in, pos, line);
       if (k == 0) return Parse::kIncomplete;
       if (k < 0) return Parse::kBad;
     }
+    r->body.reserve(static_cast<size_t>(total));
+    for (const auto& sp : spans) r->body.append(in, sp.first, sp.second);
   } else {
     int64_t n = 0;
     auto cl = r->h.find("content-length");
@@ -711,10 +716,20 @@ void on_done(IoThread& t, Done& d) {
 
 void on_readable(IoThread& t, Conn* c) {
   char buf[65536];
+  size_t since = 0;   // bytes read since the buffer was last parsed
   for (;;) {
     const ssize_t n = read(c->fd, buf, sizeof buf);
     if (n > 0) {
       c->in.append(buf, static_cast<size_t>(n));
+      since += static_cast<size_t>(n);
+      // a sender that keeps the socket readable does not grow the buffer
+      // unparsed: every MB the framing is checked (a bad line or a body over
+      // the limit closes the connection now) and complete requests dispatched
+      if (since >= (1u << 20) && !c->busy) {
+        since = 0;
+        if (!process(t, c)) return;
+        if (c->fd < 0 || c->close_after) return;   // closing once the answer is out
+      }
       continue;
     }
     if (n < 0 && errno == EINTR) continue;

@@ -201,6 +201,16 @@ def test_malformed_requests_and_framing(golden, tmp_path):
         http10,                   # HTTP/1.0: no keep-alive
         close,
     ]
+    # a 3 MB body in 4 KB chunks (arrives over many reads; the threaded parser
+    # and the application answer it), then one that closes
+    rows = [[6.8, 2.8, 4.8, 1.4], [5.0, 3.4, 1.5, 0.2]] * 70000
+    big = json.dumps({"instances": rows}).encode()
+    assert len(big) > 3_000_000
+    parts = [big[i:i + 4096] for i in range(0, len(big), 4096)]
+    big_chunked = (b"POST /v1/models/xgboost-iris:predict HTTP/1.1\r\nHost: x\r\n"
+                   b"Transfer-Encoding: chunked\r\n\r\n" +
+                   b"".join(b"%x\r\n" % len(p) + p + b"\r\n" for p in parts) + b"0\r\n\r\n")
+    cases.append(big_chunked + close)
     try:
         for data in cases:
             a = _raw(nat.port, data, timeout=3)
