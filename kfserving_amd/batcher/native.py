@@ -212,8 +212,10 @@ class NativeBatcher:
         loop = asyncio.get_running_loop()
         self._attach(loop)
         X = np.asarray(X)
+        # rows at a non-negative whole-element stride past their columns go as
+        # they are (kb_submit_convert reads the stride); anything else is copied
         if X.dtype not in (np.float32, np.float64) or X.ndim != 2 or X.strides[1] != X.itemsize \
-                or X.strides[0] % X.itemsize:
+                or X.strides[0] % X.itemsize or X.strides[0] < X.shape[1] * X.itemsize:
             X = np.ascontiguousarray(X, dtype=self._x_np)
         if X.ndim != 2 or X.shape[0] == 0:
             raise HTTPError(400, "no instances in the request")

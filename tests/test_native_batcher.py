@@ -344,3 +344,27 @@ def test_server_retires_native_batchers(golden, tmp_path):
         await asyncio.sleep(0.05)
         assert not app._batchers and second._nb._h is None
     run(go())
+
+
+def test_reversed_broadcast_and_fortran_rows():
+    """Rows at a negative or zero stride, or column-major, are copied before
+    the submit (kb_submit_convert reads a non-negative row stride)."""
+    import asyncio
+    from kfserving_amd.batcher.native import NativeBatcher
+    from kfserving_amd.forest import TI_F32
+
+    def call(X, out):
+        out[:] = X.sum(axis=1)
+        return 0
+    nb = NativeBatcher(call, 3, TI_F32, 1, TI_F32, 64, 2.0)
+
+    async def main():
+        X = np.arange(12, dtype=np.float32).reshape(4, 3)
+        for A in (X[::-1], np.broadcast_to(X[0], (5, 3)), np.asfortranarray(X),
+                  np.arange(20, dtype=np.float64).reshape(4, 5)[:, 1:4]):
+            out, _ = await nb.submit(A)
+            np.testing.assert_allclose(out, np.asarray(A, dtype=np.float32).sum(1))
+    try:
+        asyncio.run(main())
+    finally:
+        nb.close()
