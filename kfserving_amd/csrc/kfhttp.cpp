@@ -886,24 +886,33 @@ int kh_create(const kh_config* cfg, void** out) {
   auto s = std::make_unique<Server>();
   s->cfg = *cfg;
   if (s->cfg.max_body_bytes <= 0) s->cfg.max_body_bytes = 104857600;
+  // a failure part-way closes what was opened (no thread is running yet)
+  auto fail_sys = [&s]() {
+    for (auto& t : s->io) {
+      if (t->ep >= 0) close(t->ep);
+      if (t->wake >= 0) close(t->wake);
+    }
+    if (s->ffd >= 0) close(s->ffd);
+    return -3;
+  };
   s->ffd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-  if (s->ffd < 0) return -3;
+  if (s->ffd < 0) return fail_sys();
   for (int i = 0; i < cfg->io_threads; ++i) {
-    auto t = std::make_unique<IoThread>();
+    s->io.push_back(std::make_unique<IoThread>());
+    IoThread* t = s->io.back().get();
     t->srv = s.get();
     t->idx = i;
     t->ep = epoll_create1(EPOLL_CLOEXEC);
     t->wake = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-    if (t->ep < 0 || t->wake < 0) return -3;
+    if (t->ep < 0 || t->wake < 0) return fail_sys();
     epoll_event ev{};
     ev.events = EPOLLIN | EPOLLEXCLUSIVE;
     ev.data.u64 = kListen;
-    if (epoll_ctl(t->ep, EPOLL_CTL_ADD, cfg->listen_fd, &ev) != 0) return -3;
+    if (epoll_ctl(t->ep, EPOLL_CTL_ADD, cfg->listen_fd, &ev) != 0) return fail_sys();
     epoll_event wv{};
     wv.events = EPOLLIN;
     wv.data.u64 = kWake;
-    if (epoll_ctl(t->ep, EPOLL_CTL_ADD, t->wake, &wv) != 0) return -3;
-    s->io.push_back(std::move(t));
+    if (epoll_ctl(t->ep, EPOLL_CTL_ADD, t->wake, &wv) != 0) return fail_sys();
   }
   *out = s.release();
   return 0;

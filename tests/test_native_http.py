@@ -432,3 +432,22 @@ def test_lgbserver_inputs_route_bytes_equal_python_server(golden, tmp_path):
     finally:
         nat.stop()
         py.stop()
+
+
+def test_create_failure_closes_what_it_opened(tmp_path):
+    """kh_create on a descriptor epoll cannot watch (a regular file) fails
+    with -3 and leaves no descriptor of its own open."""
+    import ctypes
+    from kfserving_amd.kfserving.native_http import KH_ABI_VERSION, KhConfig
+    lib = load_library()
+    p = tmp_path / "f"
+    p.write_bytes(b"x")
+    with open(p, "rb") as fh:
+        before = len(os.listdir("/proc/self/fd"))
+        cfg = KhConfig(abi_version=KH_ABI_VERSION, listen_fd=fh.fileno(), io_threads=4,
+                       max_body_bytes=0)
+        h = ctypes.c_void_p()
+        for _ in range(5):
+            assert lib.kh_create(ctypes.byref(cfg), ctypes.byref(h)) == -3
+        assert not h.value
+        assert len(os.listdir("/proc/self/fd")) == before
