@@ -3,7 +3,7 @@ cuda:0 -- the box has one GPU -- over gloo instead of RCCL, which refuses two
 ranks on one device) run the headline and a strong-sharded C3 leg: the
 forest is created per rank, each rank predicts its own batch, rank 0 alone
 prints, value = both ranks' rows / the slowest rank's wall, C3's rows split
-in contiguous halves."""
+in contiguous halves; the C5-over-HTTP leg with two server workers."""
 import os
 import socket
 
@@ -29,7 +29,8 @@ def _rank(rank, port, q):
         args = bench.parse_args(["--steps", "4", "--warmup", "1", "--rows", "65536",
                                  "--configs", "c3", "--rows3", "200000", "--config-steps", "1",
                                  "--no-cpu-baseline", "--latency-qps", "0", "--host-rows", "0",
-                                 "--nan-variant", "0"])
+                                 "--nan-variant", "0", "--c5-http-qps", "5000",
+                                 "--c5-http-seconds", "2"])
         q.put((rank, bench.run(args, device="cuda", backend="gloo"), None))
     except Exception as e:          # surface the failure in the parent
         q.put((rank, None, repr(e)))
@@ -61,3 +62,9 @@ def test_two_ranks_one_gpu_gloo():
     ts = line["tree_shard"]
     assert ts["ranks"] == 2 and ts["rows"] == 65536 and 0 < ts["trees_rank0"] < 500
     assert ts["within_1e-5"], ts
+    # C5 over HTTP at world 2: one xgbserver worker per rank (both on this
+    # GPU here), the native front end in each, every request answered
+    c5 = line["c5_http"]
+    assert c5 is not None and "error" not in c5, c5
+    assert c5["workers"] == 2 and c5["devices"] == 2
+    assert all(p["lost"] == 0 and p["non200"] == 0 and p["requests"] > 0 for p in c5["points"])
