@@ -134,6 +134,7 @@ struct Server {
   std::deque<RouteCtx> ctxs;          // stable addresses, freed with the server
   std::atomic<uint64_t> next_thread{0};   // round robin of accepted connections
   bool started = false;
+  int parse_threads = 8;                  // KF_PARSE_THREADS, as fastjson.PARSE_THREADS
 };
 
 void signal_fd(int fd) {
@@ -529,8 +530,8 @@ void hand_to_python(IoThread& t, Conn* c, Req& r, bool keep) {
 // the fast path: true if the request went to the batcher
 bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   Server& s = *t.srv;
-  if (r.method != "POST" || r.body.size() >= KF_MT_MIN_BYTES) return false;   // big bodies: the
-  bool v2 = false;                                                           // threaded parser
+  if (r.method != "POST") return false;
+  bool v2 = false;
   const std::string name = predict_route(r.target, &v2);
   if (name.empty()) return false;
   for (const char* h : {"ce-specversion", "ce-source", "ce-type", "ce-id"})
@@ -562,28 +563,42 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   // the plugin's input checks, as flags above the element rule: a request
   // they would reject goes to the application, which answers its error
   const int rule = route.transform & 0xFF;
-  thread_local std::vector<double> xb;
-  const size_t cap = (r.body.size() + 1) / 2;
-  if (xb.size() < cap) xb.resize(cap);
+  // the parsed values: a buffer the thread keeps for small requests, one of
+  // the request's own above kKeepValues (freed with it)
+  constexpr size_t kKeepValues = size_t(1) << 19;
+  thread_local std::vector<double> xb_kept;
+  std::vector<double> xb_own;
+  std::vector<double>* xbp = &xb_kept;
+  auto reserve = [&](size_t n) {
+    xbp = n <= kKeepValues ? &xb_kept : &xb_own;
+    if (xbp->size() < n) xbp->resize(n);
+  };
+  reserve((r.body.size() + 1) / 2);   // a number takes a byte and a separator
   int64_t rows = 0, cols = 0;
   if (route.names) {   // lgbserver: {"inputs": [{column: [...]}, ...]}
+    if (r.body.size() >= KF_MT_MIN_BYTES) return false;   // the application's path
+    std::vector<double>& xb = *xbp;
     const int32_t* offs = route.name_offsets->data();
     int rc = kf_parse_inputs(r.body.data(), static_cast<int64_t>(r.body.size()),
                              route.names->data(), offs, route.n_cols, xb.data(),
                              static_cast<int64_t>(xb.size()), &rows);
     if (rc == KF_ERR_SPACE && rows > 0 && rows <= (int64_t(1) << 24)) {   // absent columns
-      xb.resize(static_cast<size_t>(rows) * route.n_cols);               // are NaN: more
+      reserve(static_cast<size_t>(rows) * route.n_cols);                 // are NaN: more
       rc = kf_parse_inputs(r.body.data(), static_cast<int64_t>(r.body.size()),   // values
-                           route.names->data(), offs, route.n_cols, xb.data(),   // than text
-                           static_cast<int64_t>(xb.size()), &rows);
+                           route.names->data(), offs, route.n_cols, xbp->data(),   // than text
+                           static_cast<int64_t>(xbp->size()), &rows);
     }
     if (rc != KF_PARSED || rows <= 0) return false;
     cols = route.n_cols;
-  } else if (kf_parse_instances(r.body.data(), static_cast<int64_t>(r.body.size()), xb.data(),
-                                static_cast<int64_t>(xb.size()), &rows, &cols) != KF_PARSED ||
+  } else if (kf_parse_instances_mt(r.body.data(), static_cast<int64_t>(r.body.size()),
+                                   xbp->data(), static_cast<int64_t>(xbp->size()), &rows, &cols,
+                                   s.parse_threads) != KF_PARSED ||
              rows <= 0 || cols != route.n_cols) {
+    // bodies of >= 1 MB on parse_threads threads, as the application's
+    // fastjson.parse_instances (KF_PARSE_THREADS)
     return false;
   }
+  const std::vector<double>& xb = *xbp;
   if (route.transform & (KH_CHECK_F32_FINITE | KH_CHECK_NO_NAN)) {
     const bool fin = route.transform & KH_CHECK_F32_FINITE, nonan = route.transform & KH_CHECK_NO_NAN;
     for (int64_t i = 0; i < rows * cols; ++i) {
@@ -886,6 +901,8 @@ int kh_create(const kh_config* cfg, void** out) {
   auto s = std::make_unique<Server>();
   s->cfg = *cfg;
   if (s->cfg.max_body_bytes <= 0) s->cfg.max_body_bytes = 104857600;
+  if (const char* e = std::getenv("KF_PARSE_THREADS"))
+    s->parse_threads = std::max(1, std::min(8, std::atoi(e)));
   // a failure part-way closes what was opened (no thread is running yet)
   auto fail_sys = [&s]() {
     for (auto& t : s->io) {

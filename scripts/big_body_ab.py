@@ -1,0 +1,92 @@
+"""Latency of large v1 :predict requests (one client, keep-alive, one at a
+time) against xgbserver with the C2 model, with the native HTTP front end and
+with the asyncio server (KF_NATIVE_HTTP=0), on the same bodies.
+
+  python scripts/big_body_ab.py [--rows 4096,65536] [--repeats 10]
+
+One JSON line per (server, rows): median / min request time and rows/s."""
+import argparse
+import http.client
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import bench_serving as bs  # noqa: E402
+
+
+def run_server(native: bool, port: int, tmp: str, rows_list, repeats: int):
+    env = dict(os.environ, KF_NATIVE_HTTP="1" if native else "0")
+    cmd = [sys.executable, "-m", "kfserving_amd.xgbserver", "--model_dir", tmp,
+           "--model_name", "model", "--http_port", str(port), "--workers", "1",
+           "--max_batchsize", "65536", "--max_latency_ms", "5", "--http_io_threads", "4"]
+    log = open(os.path.join(tmp, f"server_{int(native)}.log"), "w")
+    srv = subprocess.Popen(cmd, cwd=ROOT, env=env, start_new_session=True,
+                           stdout=subprocess.DEVNULL, stderr=log)
+    out = []
+    try:
+        if not bs.wait_ready(port, 120):
+            raise RuntimeError("server not ready")
+        bs.warm(port, 28)
+        rng = np.random.default_rng(7)
+        for rows in rows_list:
+            X = rng.standard_normal((rows, 28)).astype(np.float32)
+            body = json.dumps({"instances": X.tolist()}).encode()
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=120)
+            ts = []
+            first = None
+            for i in range(repeats + 2):
+                t0 = time.perf_counter()
+                c.request("POST", "/v1/models/model:predict", body=body,
+                          headers={"Content-Type": "application/json"})
+                r = c.getresponse()
+                data = r.read()
+                dt = time.perf_counter() - t0
+                if r.status != 200:
+                    raise RuntimeError(f"status {r.status}: {data[:200]!r}")
+                if first is None:
+                    first = json.loads(data)["predictions"]
+                if i >= 2:
+                    ts.append(dt)
+            c.close()
+            med = float(np.median(ts))
+            out.append({"server": "native front end" if native else "asyncio",
+                        "rows": rows, "body_MB": len(body) / 1e6, "median_ms": med * 1e3,
+                        "min_ms": min(ts) * 1e3, "rows_per_s": rows / med,
+                        "checksum": float(np.sum(np.asarray(first, dtype=np.float64)))})
+    finally:
+        os.killpg(srv.pid, 15)
+        srv.wait(timeout=30)
+    return out
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rows", default="4096,65536")
+    p.add_argument("--repeats", type=int, default=10)
+    p.add_argument("--port", type=int, default=18300)
+    a = p.parse_args()
+    rows_list = [int(r) for r in a.rows.split(",")]
+    tmp = tempfile.mkdtemp()
+    bs.write_c2_model(tmp)
+    res = {}
+    for rep in range(2):
+        for native in (True, False):
+            for r in run_server(native, a.port + 2 * rep + int(native), tmp, rows_list, a.repeats):
+                r["round"] = rep
+                print(json.dumps(r), flush=True)
+                res.setdefault(r["rows"], set()).add(round(r["checksum"], 6))
+    for rows, sums in res.items():   # both servers answered the same predictions
+        if len(sums) != 1:
+            raise SystemExit(f"predictions differ at {rows} rows: {sums}")
+
+
+if __name__ == "__main__":
+    main()

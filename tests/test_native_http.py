@@ -451,3 +451,30 @@ def test_create_failure_closes_what_it_opened(tmp_path):
             assert lib.kh_create(ctypes.byref(cfg), ctypes.byref(h)) == -3
         assert not h.value
         assert len(os.listdir("/proc/self/fd")) == before
+
+
+def test_large_bodies_take_the_native_route(golden, tmp_path):
+    """Bodies of >= 1 MB are parsed natively on the IO thread with the
+    threaded parser (kf_parse_instances_mt, KF_PARSE_THREADS as the
+    application's fastjson) and answered natively: the bytes equal the
+    asyncio server's, and no request reaches the application."""
+    from sklearn.datasets import load_iris
+    nat, py = _servers(golden, tmp_path, batch=65536)
+    X = load_iris()["data"]
+    rng = np.random.default_rng(4)
+    try:
+        fe = nat.server.front_end
+        for n in (50_000, 120_000):
+            rows = X[rng.integers(0, 150, n)].tolist()
+            rows[7][2] = 0                       # DMatrix(list): 0 is missing
+            body = json.dumps({"instances": rows}).encode()
+            assert len(body) >= 1 << 20
+            a = nat.fetch("/v1/models/xgboost-iris:predict", "POST", body)
+            b = py.fetch("/v1/models/xgboost-iris:predict", "POST", body)
+            assert a[0] == b[0] == 200 and dict(a[1].items()) == dict(b[1].items())
+            assert _norm(a[2]) == _norm(b[2])
+        st = fe.stats()
+        assert st["native_requests"] >= 2 and st["python_requests"] == 0
+    finally:
+        nat.stop()
+        py.stop()
