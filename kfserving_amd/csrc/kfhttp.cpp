@@ -156,55 +156,68 @@ void drain_fd(int fd) {
 // shortest round-trip digits, fixed notation when the decimal exponent is in
 // [-4, 16), else d[.ddd]e[+-]XX.
 int repr_double(double v, char* buf, int cap) {
-  std::string s;
+  char s[48];   // the longest: "-d.ddddddddddddddddde-308"
+  int n = 0;
+  auto put = [&](const char* t) {
+    while (*t) s[n++] = *t++;
+  };
   if (std::isnan(v)) {
-    s = "NaN";
+    put("NaN");
   } else if (std::isinf(v)) {
-    s = v > 0 ? "Infinity" : "-Infinity";
+    put(v > 0 ? "Infinity" : "-Infinity");
   } else if (v == 0.0) {
-    s = std::signbit(v) ? "-0.0" : "0.0";
+    put(std::signbit(v) ? "-0.0" : "0.0");
   } else {
+    // shortest round-trip digits in scientific form: [-]d[.ddd]e[+-]x
     char t[40];
-    auto r = std::to_chars(t, t + sizeof t, v, std::chars_format::scientific);
-    std::string sci(t, r.ptr);
-    bool neg = sci[0] == '-';
-    if (neg) sci.erase(0, 1);
-    const size_t e = sci.find('e');
-    std::string digits = sci.substr(0, e);
-    digits.erase(std::remove(digits.begin(), digits.end(), '.'), digits.end());
-    const int exp10 = std::atoi(sci.c_str() + e + 1);
+    const auto r = std::to_chars(t, t + sizeof t - 1, v, std::chars_format::scientific);
+    *r.ptr = '\0';   // to_chars does not terminate: atoi below reads the exponent
+    const char* p = t;
+    const char* end = r.ptr;
+    if (*p == '-') {
+      s[n++] = '-';
+      ++p;
+    }
+    char digits[24] = {};
+    int nd = 0;
+    while (p < end && *p != 'e') {
+      if (*p != '.') digits[nd++] = *p;
+      ++p;
+    }
+    const int exp10 = std::atoi(p + 1);
     const int decpt = exp10 + 1;
-    const int nd = static_cast<int>(digits.size());
-    if (neg) s += '-';
     if (decpt <= -4 || decpt > 16) {
-      s += digits[0];
+      s[n++] = digits[0];
       if (nd > 1) {
-        s += '.';
-        s.append(digits, 1, std::string::npos);
+        s[n++] = '.';
+        for (int k = 1; k < nd; ++k) s[n++] = digits[k];
       }
-      s += 'e';
-      s += exp10 < 0 ? '-' : '+';
+      s[n++] = 'e';
+      s[n++] = exp10 < 0 ? '-' : '+';
       const int a = std::abs(exp10);
-      if (a < 10) s += '0';
-      s += std::to_string(a);
+      if (a >= 100) s[n++] = static_cast<char>('0' + a / 100);
+      s[n++] = static_cast<char>('0' + (a / 10) % 10);
+      s[n++] = static_cast<char>('0' + a % 10);
     } else if (decpt <= 0) {
-      s += "0.";
-      s.append(static_cast<size_t>(-decpt), '0');
-      s += digits;
+      s[n++] = '0';
+      s[n++] = '.';
+      for (int k = 0; k < -decpt; ++k) s[n++] = '0';
+      for (int k = 0; k < nd; ++k) s[n++] = digits[k];
     } else if (decpt >= nd) {
-      s += digits;
-      s.append(static_cast<size_t>(decpt - nd), '0');
-      s += ".0";
+      for (int k = 0; k < nd; ++k) s[n++] = digits[k];
+      for (int k = nd; k < decpt; ++k) s[n++] = '0';
+      s[n++] = '.';
+      s[n++] = '0';
     } else {
-      s.append(digits, 0, static_cast<size_t>(decpt));
-      s += '.';
-      s.append(digits, static_cast<size_t>(decpt), std::string::npos);
+      for (int k = 0; k < decpt; ++k) s[n++] = digits[k];
+      s[n++] = '.';
+      for (int k = decpt; k < nd; ++k) s[n++] = digits[k];
     }
   }
-  if (static_cast<int>(s.size()) >= cap) return -1;
-  std::memcpy(buf, s.data(), s.size());
-  buf[s.size()] = '\0';
-  return static_cast<int>(s.size());
+  if (n >= cap) return -1;
+  std::memcpy(buf, s, static_cast<size_t>(n));
+  buf[n] = '\0';
+  return n;
 }
 
 void append_double(std::string& o, double v) {
@@ -567,38 +580,43 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   // the request's own above kKeepValues (freed with it)
   constexpr size_t kKeepValues = size_t(1) << 19;
   thread_local std::vector<double> xb_kept;
-  std::vector<double> xb_own;
-  std::vector<double>* xbp = &xb_kept;
+  std::unique_ptr<double[]> xb_own;   // not value-initialised: the parser writes it
+  double* xb = nullptr;
+  size_t xb_n = 0;
   auto reserve = [&](size_t n) {
-    xbp = n <= kKeepValues ? &xb_kept : &xb_own;
-    if (xbp->size() < n) xbp->resize(n);
+    if (n <= kKeepValues) {
+      if (xb_kept.size() < n) xb_kept.resize(n);
+      xb = xb_kept.data();
+    } else {
+      xb_own.reset(new double[n]);
+      xb = xb_own.get();
+    }
+    xb_n = n;
   };
   reserve((r.body.size() + 1) / 2);   // a number takes a byte and a separator
   int64_t rows = 0, cols = 0;
   if (route.names) {   // lgbserver: {"inputs": [{column: [...]}, ...]}
     if (r.body.size() >= KF_MT_MIN_BYTES) return false;   // the application's path
-    std::vector<double>& xb = *xbp;
     const int32_t* offs = route.name_offsets->data();
     int rc = kf_parse_inputs(r.body.data(), static_cast<int64_t>(r.body.size()),
-                             route.names->data(), offs, route.n_cols, xb.data(),
-                             static_cast<int64_t>(xb.size()), &rows);
+                             route.names->data(), offs, route.n_cols, xb,
+                             static_cast<int64_t>(xb_n), &rows);
     if (rc == KF_ERR_SPACE && rows > 0 && rows <= (int64_t(1) << 24)) {   // absent columns
       reserve(static_cast<size_t>(rows) * route.n_cols);                 // are NaN: more
       rc = kf_parse_inputs(r.body.data(), static_cast<int64_t>(r.body.size()),   // values
-                           route.names->data(), offs, route.n_cols, xbp->data(),   // than text
-                           static_cast<int64_t>(xbp->size()), &rows);
+                           route.names->data(), offs, route.n_cols, xb,   // than text
+                           static_cast<int64_t>(xb_n), &rows);
     }
     if (rc != KF_PARSED || rows <= 0) return false;
     cols = route.n_cols;
   } else if (kf_parse_instances_mt(r.body.data(), static_cast<int64_t>(r.body.size()),
-                                   xbp->data(), static_cast<int64_t>(xbp->size()), &rows, &cols,
+                                   xb, static_cast<int64_t>(xb_n), &rows, &cols,
                                    s.parse_threads) != KF_PARSED ||
              rows <= 0 || cols != route.n_cols) {
     // bodies of >= 1 MB on parse_threads threads, as the application's
     // fastjson.parse_instances (KF_PARSE_THREADS)
     return false;
   }
-  const std::vector<double>& xb = *xbp;
   if (route.transform & (KH_CHECK_F32_FINITE | KH_CHECK_NO_NAN)) {
     const bool fin = route.transform & KH_CHECK_F32_FINITE, nonan = route.transform & KH_CHECK_NO_NAN;
     for (int64_t i = 0; i < rows * cols; ++i) {
@@ -613,7 +631,7 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   c->res.assign(static_cast<size_t>(rows) * route.out_width * route.out_elem, 0);
   c->busy = true;
   const uint64_t tag = KB_TAG_CALLBACK | (static_cast<uint64_t>(t.idx) << kThreadShift) | c->id;
-  if (kb_submit_convert(route.batcher, xb.data(), 1, rows, cols, rule, c->res.data(),
+  if (kb_submit_convert(route.batcher, xb, 1, rows, cols, rule, c->res.data(),
                         tag) != KB_OK) {
     c->busy = false;   // the batcher was retired meanwhile: the application answers
     return false;

@@ -27,7 +27,9 @@ def run_server(native: bool, port: int, tmp: str, rows_list, repeats: int):
     cmd = [sys.executable, "-m", "kfserving_amd.xgbserver", "--model_dir", tmp,
            "--model_name", "model", "--http_port", str(port), "--workers", "1",
            "--max_batchsize", "65536", "--max_latency_ms", "5", "--http_io_threads", "4"]
-    log = open(os.path.join(tmp, f"server_{int(native)}.log"), "w")
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    log_path = os.path.join(ROOT, "gpurun_out", f"big_body_server_{int(native)}_{port}.log")
+    log = open(log_path, "w")
     srv = subprocess.Popen(cmd, cwd=ROOT, env=env, start_new_session=True,
                            stdout=subprocess.DEVNULL, stderr=log)
     out = []
@@ -61,8 +63,13 @@ def run_server(native: bool, port: int, tmp: str, rows_list, repeats: int):
                         "rows": rows, "body_MB": len(body) / 1e6, "median_ms": med * 1e3,
                         "min_ms": min(ts) * 1e3, "rows_per_s": rows / med,
                         "checksum": float(np.sum(np.asarray(first, dtype=np.float64)))})
+    except Exception:
+        print(f"[{'native' if native else 'asyncio'}] server exit code {srv.poll()}, log "
+              f"{log_path}", file=sys.stderr, flush=True)
+        raise
     finally:
-        os.killpg(srv.pid, 15)
+        if srv.poll() is None:
+            os.killpg(srv.pid, 15)
         srv.wait(timeout=30)
     return out
 
