@@ -413,7 +413,8 @@ struct Req {
   std::string method, target, version, headers;   // headers: "k: v\n" lines
   std::unordered_map<std::string, std::string> h;
   std::string body;
-  size_t end = 0;   // bytes of the read buffer it used
+  size_t end = 0;    // bytes of the read buffer it used
+  size_t need = 0;   // kIncomplete with a Content-Length: the request's whole size
 };
 
 Parse parse_request(const std::string& in, size_t start, int64_t max_body, Req* r) {
@@ -487,7 +488,10 @@ Parse parse_request(const std::string& in, size_t start, int64_t max_body, Req* 
     if (cl != r->h.end() && !cl->second.empty() && !py_int(cl->second, 10, &n)) return Parse::kBad;
     if (n > max_body) return Parse::kTooLarge;
     if (n < 0) return Parse::kBad;
-    if (in.size() - pos < static_cast<size_t>(n)) return Parse::kIncomplete;
+    if (in.size() - pos < static_cast<size_t>(n)) {
+      r->need = pos - start + static_cast<size_t>(n);
+      return Parse::kIncomplete;
+    }
     r->body.assign(in, pos, static_cast<size_t>(n));
     pos += static_cast<size_t>(n);
   }
@@ -705,6 +709,11 @@ bool process(IoThread& t, Conn* c) {
         c->in.erase(0, c->in_off);
         c->in_off = 0;
       }
+      // a large body, once its first MB is here, arrives into room for all of
+      // it (no re-copy as the buffer grows)
+      if (r.need > (1u << 20) && c->in.size() - c->in_off >= (1u << 20) &&
+          c->in.capacity() < c->in_off + r.need)
+        c->in.reserve(c->in_off + r.need);
       return true;
     }
     if (p == Parse::kBad || p == Parse::kTooLarge) {
