@@ -66,3 +66,51 @@ def test_native_http_c2_bytes_equal_python_server(tmp_path):
     finally:
         nat.stop()
         py.stop()
+
+
+def test_native_http_c2_large_bodies(tmp_path):
+    """v1 bodies of 2.4 and 38 MB (4,096 and 65,536 rows) take the native
+    route on the GPU (the threaded parser on the IO thread): the bytes equal
+    the asyncio server's, no request reaches the application, and the
+    probabilities are the oracle's."""
+    import bench_serving as bs
+    from kfserving_amd.xgbserver import XGBoostModel
+    from oracle import xgb_ref
+    bs.write_c2_model(str(tmp_path))
+    runs = []
+    for native in (True, False):
+        m = XGBoostModel("model", str(tmp_path), 1)
+        assert m.load()
+        srv = KFServer(max_batchsize=65536, max_latency_ms=3)
+        srv.native_http = native
+        srv.register_model(m)
+        runs.append(_Running(srv))
+    nat, py = runs
+    t0 = time.time()
+    while nat.server.front_end is None and time.time() - t0 < 60:
+        time.sleep(0.05)
+    ref = xgb_ref.read_xgb_binary(os.path.join(str(tmp_path), "model.bst"))
+    rng = np.random.default_rng(11)
+    try:
+        small = json.dumps({"instances": rng.standard_normal((4, 28)).tolist()}).encode()
+        assert nat.fetch("/v1/models/model:predict", "POST", small)[0] == 200   # the route
+        assert "model" in nat.server.front_end.routes
+        before = nat.server.front_end.stats()
+        for rows in (4096, 65536):
+            X = rng.standard_normal((rows, 28)).astype(np.float32)
+            X[rng.random(X.shape) < 0.02] = 0.0           # DMatrix(list): missing
+            body = json.dumps({"instances": X.tolist()}).encode()
+            a = nat.fetch("/v1/models/model:predict", "POST", body)
+            b = py.fetch("/v1/models/model:predict", "POST", body)
+            assert a[0] == b[0] == 200 and a[1] == b[1]
+            assert _norm(a[2]) == _norm(b[2])
+            got = np.asarray(json.loads(a[2])["predictions"])
+            Xo = X.copy()
+            Xo[X == 0] = np.nan
+            np.testing.assert_allclose(got[:2000], xgb_ref.predict(ref, Xo[:2000]), rtol=1e-5, atol=0)
+        st = nat.server.front_end.stats()
+        assert st["native_requests"] - before["native_requests"] == 2
+        assert st["python_requests"] == before["python_requests"]
+    finally:
+        nat.stop()
+        py.stop()
