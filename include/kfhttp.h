@@ -94,6 +94,19 @@ int kh_add_v1_inputs_predict(void* srv, const char* model, void* batcher, int32_
                              int32_t out_width, int32_t out_elem_bytes, const char* names,
                              const int32_t* name_offsets);
 
+/* Answer V2 tensor requests on POST /v2/models/<model>/infer natively through
+ * `batcher` (the model's batcher of V2 tensor rows): a body kf_parse_v2_tensor
+ * takes, of n_cols columns, is converted to the batcher's type as numpy casts
+ * it (FP32 data rounded to float32 first) and answered as
+ * kfserving_amd/kfserving/v2.py encode_response answers it:
+ * {"model_name": ..., ["id": ...,] "outputs": [{"name": "predict", "shape":
+ * [N] or [N, out_width], "datatype": "FP32" | "FP64", "data": [...]}]}.
+ * Every other V2 request (binary tensor data, "outputs", other datatypes, ...)
+ * goes to the application.  The route is removed with
+ * kh_remove_route(srv, "v2:<model>"). */
+int kh_add_v2_tensor_predict(void* srv, const char* model, void* batcher, int32_t n_cols,
+                             int32_t out_width, int32_t out_elem_bytes);
+
 /* Stop answering the model natively (its requests go to the application):
  * the batcher's forming batch is flushed, the requests already submitted are
  * answered, and the batcher's done callback is detached before this returns,

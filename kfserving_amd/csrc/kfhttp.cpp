@@ -65,6 +65,7 @@ struct Route {
   // columns by these names (back to back, offsets n_cols + 1)
   std::shared_ptr<const std::string> names;
   std::shared_ptr<const std::vector<int32_t>> name_offsets;
+  bool v2 = false;   // V2 tensor requests (kh_add_v2_tensor_predict)
 };
 
 struct Conn {
@@ -83,6 +84,7 @@ struct Conn {
   std::vector<unsigned char> res;
   int64_t rows = 0;
   bool keep = true;
+  std::string model, v2_id;   // a V2 tensor answer: the model's name, the request's id text
   // the request handed to Python (kept until kh_respond)
   std::string method, target, version, headers, body;
 };
@@ -554,18 +556,17 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   for (const char* h : {"ce-specversion", "ce-source", "ce-type", "ce-id"})
     if (r.h.count(h)) return false;   // binary CloudEvents: the application's path
   // /v2/.../infer answers a v1 body as :predict does (ref kfserver.py:77-78);
-  // a V2 tensor request (a binary tail, or a "datatype" in the body) is the
-  // application's
-  if (v2 && (r.h.count("inference-header-content-length") ||
-             r.body.find("\"datatype\"") != std::string::npos))
-    return false;
+  // a V2 tensor request (a "datatype" in the body) takes the model's V2
+  // route if it has one, and binary tensor data is the application's
+  if (v2 && r.h.count("inference-header-content-length")) return false;
+  const bool tensor = v2 && r.body.find("\"datatype\"") != std::string::npos;
   Route route;
   {
     // the reservation is taken under the route lock: kh_remove_route erases
     // the route under it and then waits for every reservation, so the batcher
     // cannot be destroyed between this lookup and the submit below
     std::lock_guard<std::mutex> lk(s.rmu);
-    auto it = s.routes.find(name);
+    auto it = s.routes.find(tensor ? "v2:" + name : name);
     if (it == s.routes.end()) return false;
     route = it->second;
     route.ctx->inflight.fetch_add(1);
@@ -599,7 +600,21 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   };
   reserve((r.body.size() + 1) / 2);   // a number takes a byte and a separator
   int64_t rows = 0, cols = 0;
-  if (route.names) {   // lgbserver: {"inputs": [{column: [...]}, ...]}
+  int32_t x_dtype = 1;   // the rows handed to the batcher: float64 (0: float32)
+  int64_t id_off = 0, id_len = 0;
+  if (tensor) {   // {"inputs": [{"name", "shape", "datatype", "data"}], "id"}
+    int32_t dt = -1;
+    if (kf_parse_v2_tensor(r.body.data(), static_cast<int64_t>(r.body.size()), xb,
+                           static_cast<int64_t>(xb_n), &rows, &cols, &dt, &id_off,
+                           &id_len) != KF_PARSED ||
+        cols != route.n_cols)
+      return false;   // the application: v2.decode_inputs, or an unbatched predict
+    if (dt == 0) {    // np.asarray(data, float32): each value rounded to float32
+      float* f = reinterpret_cast<float*>(xb);   // in place, front to back
+      for (int64_t i = 0; i < rows * cols; ++i) f[i] = static_cast<float>(xb[i]);
+      x_dtype = 0;
+    }
+  } else if (route.names) {   // lgbserver: {"inputs": [{column: [...]}, ...]}
     if (r.body.size() >= KF_MT_MIN_BYTES) return false;   // the application's path
     const int32_t* offs = route.name_offsets->data();
     int rc = kf_parse_inputs(r.body.data(), static_cast<int64_t>(r.body.size()),
@@ -623,8 +638,9 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   }
   if (route.transform & (KH_CHECK_F32_FINITE | KH_CHECK_NO_NAN)) {
     const bool fin = route.transform & KH_CHECK_F32_FINITE, nonan = route.transform & KH_CHECK_NO_NAN;
+    const float* f = reinterpret_cast<const float*>(xb);
     for (int64_t i = 0; i < rows * cols; ++i) {
-      const double v = xb[static_cast<size_t>(i)];
+      const double v = x_dtype == 0 ? f[i] : xb[static_cast<size_t>(i)];
       if (nonan && std::isnan(v)) return false;
       if (fin && std::isinf(static_cast<float>(v))) return false;
     }
@@ -632,10 +648,14 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   c->route = route;
   c->rows = rows;
   c->keep = keep;
+  if (tensor) {
+    c->model = name;
+    c->v2_id.assign(r.body, static_cast<size_t>(id_off), static_cast<size_t>(id_len));
+  }
   c->res.assign(static_cast<size_t>(rows) * route.out_width * route.out_elem, 0);
   c->busy = true;
   const uint64_t tag = KB_TAG_CALLBACK | (static_cast<uint64_t>(t.idx) << kThreadShift) | c->id;
-  if (kb_submit_convert(route.batcher, xb, 1, rows, cols, rule, c->res.data(),
+  if (kb_submit_convert(route.batcher, xb, x_dtype, rows, cols, rule, c->res.data(),
                         tag) != KB_OK) {
     c->busy = false;   // the batcher was retired meanwhile: the application answers
     return false;
@@ -647,7 +667,63 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
 
 // the Python server's bytes for a batched :predict (NativeModelBatcher.submit
 // -> model.postprocess -> _ok -> _json_body)
+// kfserver.infer's bytes for a V2 tensor request (v2.encode_response: the
+// model's output under "predict" in its own datatype, json.dumps of it), or
+// for a failed batch HTTPError(500, "Failed to predict ...") as
+// error_response renders it
+void answer_v2(Conn* c, const kb_completion& d, const std::string& err) {
+  std::string body;
+  if (d.status != KB_OK) {
+    const std::string reason = "Failed to predict " + err;
+    std::string line = reason;
+    for (char& ch : line)
+      if (ch == '\r' || ch == '\n') ch = ' ';   // status_reason
+    body = "<html><title>500: " + reason + "</title><body>500: " + reason + "</body></html>";
+    append_response(c->out, 500, line.c_str(), "text/html; charset=UTF-8", body, c->keep);
+  } else {
+    const int w = c->route.out_width;
+    body.reserve(128 + static_cast<size_t>(c->rows) * w * 22);
+    body += "{\"model_name\": \"";
+    body += c->model;
+    body += '"';
+    if (!c->v2_id.empty()) {
+      body += ", \"id\": ";
+      body += c->v2_id;
+    }
+    body += ", \"outputs\": [{\"name\": \"predict\", \"shape\": [";
+    body += std::to_string(c->rows);
+    if (w > 1) {
+      body += ", ";
+      body += std::to_string(w);
+    }
+    body += c->route.out_elem == 4 ? "], \"datatype\": \"FP32\", \"data\": [" : "], \"datatype\": \"FP64\", \"data\": [";
+    const size_t n = static_cast<size_t>(c->rows) * w;
+    for (size_t i = 0; i < n; ++i) {
+      if (i) body += ", ";
+      double v;
+      if (c->route.out_elem == 4) {
+        float f;
+        std::memcpy(&f, c->res.data() + i * 4, 4);
+        v = f;
+      } else {
+        std::memcpy(&v, c->res.data() + i * 8, 8);
+      }
+      append_double(body, v);
+    }
+    body += "]}]}";
+    append_response(c->out, 200, "OK", "application/json", body, c->keep);
+  }
+  c->close_after = c->close_after || !c->keep;
+  std::vector<unsigned char>().swap(c->res);
+  c->model.clear();
+  c->v2_id.clear();
+}
+
 void answer_native(Conn* c, const kb_completion& d, const std::string& err) {
+  if (c->route.v2) {
+    answer_v2(c, d, err);
+    return;
+  }
   std::string body;
   body.reserve(64 + static_cast<size_t>(c->rows) * c->route.out_width * 22);
   if (d.status == KB_OK) {
@@ -965,16 +1041,17 @@ int kh_create(const kh_config* cfg, void** out) {
 static int add_route(void* h, const char* model, void* batcher, int32_t n_cols,
                      int32_t out_width, int32_t out_elem_bytes, int32_t transform,
                      const char* labels, const int32_t* label_offsets, int32_t n_labels,
-                     const char* names, const int32_t* name_offsets) {
+                     const char* names, const int32_t* name_offsets, bool v2 = false) {
   if (!h || !model || !batcher || n_cols <= 0 || out_width <= 0 ||
       (out_elem_bytes != 4 && out_elem_bytes != 8) || n_labels < 0 ||
       (n_labels > 0 && (!labels || !label_offsets || out_width != 1)))
     return -1;
   Server& s = *static_cast<Server*>(h);
+  const std::string key = v2 ? "v2:" + std::string(model) : std::string(model);
   RouteCtx* ctx;
   {
     std::lock_guard<std::mutex> lk(s.rmu);
-    if (s.routes.count(model)) return -1;   // remove the old route first (kh_remove_route)
+    if (s.routes.count(key)) return -1;   // remove the old route first (kh_remove_route)
     s.ctxs.emplace_back();
     ctx = &s.ctxs.back();
     ctx->s = &s;
@@ -1000,8 +1077,9 @@ static int add_route(void* h, const char* model, void* batcher, int32_t n_cols,
     r.name_offsets = std::make_shared<const std::vector<int32_t>>(name_offsets,
                                                                   name_offsets + n_cols + 1);
   }
+  r.v2 = v2;
   std::lock_guard<std::mutex> lk(s.rmu);
-  s.routes[model] = r;
+  s.routes[key] = r;
   return 0;
 }
 
@@ -1018,6 +1096,12 @@ int kh_add_v1_inputs_predict(void* h, const char* model, void* batcher, int32_t 
   if (!names || !name_offsets) return -1;
   return add_route(h, model, batcher, n_cols, out_width, out_elem_bytes, KB_IN_PLAIN, nullptr,
                    nullptr, 0, names, name_offsets);
+}
+
+int kh_add_v2_tensor_predict(void* h, const char* model, void* batcher, int32_t n_cols,
+                             int32_t out_width, int32_t out_elem_bytes) {
+  return add_route(h, model, batcher, n_cols, out_width, out_elem_bytes, KB_IN_PLAIN, nullptr,
+                   nullptr, 0, nullptr, nullptr, true);
 }
 
 int kh_remove_route(void* h, const char* model) {

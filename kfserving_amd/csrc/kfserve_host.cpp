@@ -611,3 +611,193 @@ extern "C" int kf_parse_inputs(const char* body, int64_t len, const char* names,
   *rows = R;
   return overflow ? KF_ERR_SPACE : KF_PARSED;
 }
+
+// --------------------------------------------------- V2 inference tensors
+namespace {
+
+// a JSON string of printable ASCII without escapes at sc.p ('"' included):
+// its text is then the same after json.loads + json.dumps; anything else
+// (escapes, controls, non-ASCII) is left to the application
+bool plain_string(Scanner& sc, const char** s, int64_t* n) {
+  if (!sc.eat('"')) return false;
+  const char* a = sc.p;
+  while (sc.p < sc.end && *sc.p != '"') {
+    const unsigned char ch = static_cast<unsigned char>(*sc.p);
+    if (ch < 0x20 || ch > 0x7E || ch == '\\') return false;
+    ++sc.p;
+  }
+  if (sc.p >= sc.end) return false;
+  *s = a - 1;
+  *n = (sc.p - a) + 2;
+  ++sc.p;
+  return true;
+}
+
+// a Python int as a V2 shape entry: digits only (no sign, fraction, exponent)
+bool shape_int(Scanner& sc, int64_t* v) {
+  if (sc.p >= sc.end || !Scanner::digit(*sc.p)) return false;
+  if (*sc.p == '0' && sc.end - sc.p > 1 && Scanner::digit(sc.p[1])) return false;   // "01"
+  int64_t x = 0;
+  int nd = 0;
+  while (sc.p < sc.end && Scanner::digit(*sc.p)) {
+    if (++nd > 12) return false;
+    x = x * 10 + (*sc.p++ - '0');
+  }
+  *v = x;
+  return true;
+}
+
+// "data": numbers, flat or one level of equal-length rows (np.asarray of
+// it is then a 1- or 2-D array of the same values in the same order)
+bool tensor_data(Scanner& sc, double* out, int64_t cap, int64_t* n) {
+  if (!sc.eat('[')) return false;
+  sc.ws();
+  if (sc.p < sc.end && *sc.p == ']') return false;   // empty: the application
+  const bool nested = sc.p < sc.end && *sc.p == '[';
+  int64_t k = 0, width = -1;
+  for (;;) {
+    sc.ws();
+    if (nested) {
+      if (!sc.eat('[')) return false;
+      int64_t w = 0;
+      for (;;) {
+        sc.ws();
+        double v;
+        if (!sc.number(&v)) return false;
+        if (k < cap) out[k] = v;
+        ++k;
+        ++w;
+        sc.ws();
+        if (sc.eat(',')) continue;
+        if (sc.eat(']')) break;
+        return false;
+      }
+      if (width < 0) width = w;
+      else if (w != width) return false;   // ragged: numpy's error
+    } else {
+      double v;
+      if (!sc.number(&v)) return false;
+      if (k < cap) out[k] = v;
+      ++k;
+    }
+    sc.ws();
+    if (sc.eat(',')) continue;
+    if (sc.eat(']')) break;
+    return false;
+  }
+  *n = k;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int kf_parse_v2_tensor(const char* body, int64_t len, double* out, int64_t cap,
+                                  int64_t* rows, int64_t* cols, int32_t* datatype,
+                                  int64_t* id_off, int64_t* id_len) {
+  if (!body || len < 0 || !rows || !cols || !datatype || !id_off || !id_len) return KF_FALLBACK;
+  *rows = *cols = 0;
+  *datatype = -1;
+  *id_off = *id_len = 0;
+  Scanner sc{body, body + len};
+  bool seen_inputs = false, seen_id = false, overflow = false;
+  int64_t shape[2] = {0, 0}, ndim = -1, count = -1;
+  sc.ws();
+  if (!sc.eat('{')) return KF_FALLBACK;
+  for (;;) {   // the request's keys: "inputs" and "id" only
+    sc.ws();
+    if (sc.lit("\"inputs\"", 8)) {
+      if (seen_inputs) return KF_FALLBACK;
+      seen_inputs = true;
+      sc.ws();
+      if (!sc.eat(':')) return KF_FALLBACK;
+      sc.ws();
+      if (!sc.eat('[')) return KF_FALLBACK;
+      sc.ws();
+      if (!sc.eat('{')) return KF_FALLBACK;   // exactly one tensor
+      bool s_name = false, s_shape = false, s_type = false, s_data = false;
+      for (;;) {
+        sc.ws();
+        if (sc.lit("\"name\"", 6)) {
+          if (s_name) return KF_FALLBACK;
+          s_name = true;
+          sc.ws();
+          if (!sc.eat(':')) return KF_FALLBACK;
+          sc.ws();
+          const char* s;
+          int64_t n;
+          if (!plain_string(sc, &s, &n)) return KF_FALLBACK;
+        } else if (sc.lit("\"shape\"", 7)) {
+          if (s_shape) return KF_FALLBACK;
+          s_shape = true;
+          sc.ws();
+          if (!sc.eat(':')) return KF_FALLBACK;
+          sc.ws();
+          if (!sc.eat('[')) return KF_FALLBACK;
+          ndim = 0;
+          for (;;) {
+            sc.ws();
+            int64_t d;
+            if (ndim >= 2 || !shape_int(sc, &d)) return KF_FALLBACK;
+            shape[ndim++] = d;
+            sc.ws();
+            if (sc.eat(',')) continue;
+            if (sc.eat(']')) break;
+            return KF_FALLBACK;
+          }
+        } else if (sc.lit("\"datatype\"", 10)) {
+          if (s_type) return KF_FALLBACK;
+          s_type = true;
+          sc.ws();
+          if (!sc.eat(':')) return KF_FALLBACK;
+          sc.ws();
+          if (sc.lit("\"FP32\"", 6)) *datatype = 0;
+          else if (sc.lit("\"FP64\"", 6)) *datatype = 1;
+          else return KF_FALLBACK;
+        } else if (sc.lit("\"data\"", 6)) {
+          if (s_data) return KF_FALLBACK;
+          s_data = true;
+          sc.ws();
+          if (!sc.eat(':')) return KF_FALLBACK;
+          sc.ws();
+          if (!tensor_data(sc, out, cap, &count)) return KF_FALLBACK;
+          if (count > cap) overflow = true;
+        } else {
+          return KF_FALLBACK;   // "parameters" (binary data) and the rest: the application
+        }
+        sc.ws();
+        if (sc.eat(',')) continue;
+        if (sc.eat('}')) break;
+        return KF_FALLBACK;
+      }
+      if (!(s_shape && s_type && s_data)) return KF_FALLBACK;
+      sc.ws();
+      if (!sc.eat(']')) return KF_FALLBACK;   // a second tensor: the application
+    } else if (sc.lit("\"id\"", 4)) {
+      if (seen_id) return KF_FALLBACK;
+      seen_id = true;
+      sc.ws();
+      if (!sc.eat(':')) return KF_FALLBACK;
+      sc.ws();
+      const char* s;
+      int64_t n;
+      if (!plain_string(sc, &s, &n)) return KF_FALLBACK;
+      *id_off = s - body;
+      *id_len = n;
+    } else {
+      return KF_FALLBACK;   // "outputs", "parameters", ...: the application
+    }
+    sc.ws();
+    if (sc.eat(',')) continue;
+    if (sc.eat('}')) break;
+    return KF_FALLBACK;
+  }
+  sc.ws();
+  if (sc.p != sc.end || !seen_inputs) return KF_FALLBACK;
+  // np.asarray(data).size == prod(shape), reshaped; a [F] tensor is one row
+  const int64_t r = ndim == 1 ? 1 : shape[0];
+  const int64_t c = ndim == 1 ? shape[0] : shape[1];
+  if (ndim < 1 || r <= 0 || c <= 0 || r * c != count) return KF_FALLBACK;
+  *rows = r;
+  *cols = c;
+  return overflow ? KF_ERR_SPACE : KF_PARSED;
+}

@@ -26,7 +26,7 @@ from .kfmodel import KFModel
 KH_ABI_VERSION = 1
 
 EXPORTED_SYMBOLS = ("kh_create", "kh_add_v1_predict", "kh_add_v1_inputs_predict",
-                    "kh_remove_route", "kh_start",
+                    "kh_add_v2_tensor_predict", "kh_remove_route", "kh_start",
                     "kh_fallback_fd", "kh_next_fallback", "kh_respond", "kh_get_stats",
                     "kh_destroy", "kh_repr_double", "kh_abi_version")
 
@@ -72,6 +72,8 @@ def load_library() -> ctypes.CDLL:
     lib.kh_add_v1_inputs_predict.restype = ctypes.c_int
     lib.kh_add_v1_inputs_predict.argtypes = [vp, ctypes.c_char_p, vp, i32, i32, i32,
                                              ctypes.c_char_p, ctypes.POINTER(i32)]
+    lib.kh_add_v2_tensor_predict.restype = ctypes.c_int
+    lib.kh_add_v2_tensor_predict.argtypes = [vp, ctypes.c_char_p, vp, i32, i32, i32]
     lib.kh_remove_route.restype = ctypes.c_int
     lib.kh_remove_route.argtypes = [vp, ctypes.c_char_p]
     lib.kh_start.restype = ctypes.c_int
@@ -201,7 +203,12 @@ class NativeFrontEnd:
             self.routes[name] = h
 
     def _on_batcher(self, event: str, name: str, kind: str, batcher) -> None:
-        if kind not in ("instances", "inputs") or self._h is None:
+        if self._h is None:
+            return
+        if kind == "tensor":
+            self._on_tensor_batcher(event, name, batcher)
+            return
+        if kind not in ("instances", "inputs"):
             return
         model = batcher.model
         if kind != route_kind(model):
@@ -216,6 +223,27 @@ class NativeFrontEnd:
                 spec = _spec_of(batcher, model)
                 if spec is not None:
                     self._register(name, spec)
+
+    def _on_tensor_batcher(self, event: str, name: str, batcher) -> None:
+        """V2 tensor requests (/v2/models/<name>/infer with "datatype") of a
+        plugin that declares ``native_v2_tensor`` go natively through the
+        model's tensor batcher, which the application makes on the first
+        such request (route key "v2:<name>")."""
+        key = "v2:" + name
+        if event == "retire" and key in self.routes:
+            self._lib.kh_remove_route(self._h, key.encode())
+            del self.routes[key]
+        elif event == "create" and key not in self.routes:
+            model = batcher.model
+            if not getattr(model, "native_v2_tensor", False) or \
+                    not route_spec_static(self.app, model):
+                return
+            spec = _spec_of(batcher, model)
+            if spec is None:
+                return
+            h, F, w, e = spec[:4]
+            if self._lib.kh_add_v2_tensor_predict(self._h, name.encode(), h, F, w, e) == 0:
+                self.routes[key] = h
 
     def stats(self) -> dict:
         st = KhStats()

@@ -54,6 +54,9 @@ class XGBoostModel(GPUForestMixin, KFModel):
     # the native HTTP front end answers batched v1 :predict bodies of this
     # model itself, with DMatrix(list)'s element rule (kfbatch.h KB_IN_XGB_LIST)
     native_v1_transform = 1
+    # ... and its V2 tensor requests (FP32 / FP64 JSON data, kh_add_v2_tensor_predict):
+    # tensor_matrix is the plain float32 cast the native batcher applies
+    native_v2_tensor = True
 
     def native_request(self, chunk, kind: str):
         # a natively decoded JSON list: DMatrix(list)'s rule (0 missing, NaN

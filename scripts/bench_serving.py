@@ -46,14 +46,28 @@ KFServer(http_port=%(port)d, workers=%(workers)d, max_batchsize=%(mbs)d,
 '''
 
 
-def write_bodies(path, n_feat, variants, seed):
+def body_of(X, protocol="v1"):
+    """A request of rows X: v1 {"instances": rows}, or a V2 inference request
+    with one FP32 tensor of JSON data (docs/predict-api/v2/required_api.md)."""
+    if protocol == "v2":
+        return json.dumps({"inputs": [{"name": "input-0", "shape": list(X.shape),
+                                       "datatype": "FP32",
+                                       "data": X.reshape(-1).tolist()}]}).encode()
+    return json.dumps({"instances": X.tolist()}).encode()
+
+
+def predict_path(protocol="v1", model="model"):
+    return f"/v2/models/{model}/infer" if protocol == "v2" else f"/v1/models/{model}:predict"
+
+
+def write_bodies(path, n_feat, variants, seed, protocol="v1"):
     rng = np.random.default_rng(seed)
     with open(path, "wb") as fh:
         fh.write(struct.pack("<I", variants))
         for r in range(1, 65):
             for _ in range(variants):
                 X = rng.standard_normal((r, n_feat), dtype=np.float32)
-                b = json.dumps({"instances": X.tolist()}).encode()
+                b = body_of(X, protocol)
                 fh.write(struct.pack("<I", len(b)))
                 fh.write(b)
 
@@ -83,11 +97,11 @@ def wait_ready(port, timeout=180):
     return False
 
 
-def warm(port, n_feat, n=20):
-    body = json.dumps({"instances": np.zeros((64, n_feat)).tolist()}).encode()
+def warm(port, n_feat, n=20, protocol="v1"):
+    body = body_of(np.zeros((64, n_feat), dtype=np.float32), protocol)
     for _ in range(n):
         c = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
-        c.request("POST", "/v1/models/model:predict", body=body,
+        c.request("POST", predict_path(protocol), body=body,
                   headers={"Content-Type": "application/json"})
         r = c.getresponse()
         r.read()
@@ -98,7 +112,7 @@ def warm(port, n_feat, n=20):
 
 def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.0, conns=4096,
                       port=18080, model="c2", max_batch=65536, max_latency_ms=5, env=None,
-                      ready_timeout=180, loadgen_threads=1, echo=True):
+                      ready_timeout=180, loadgen_threads=1, echo=True, protocol="v1"):
     """Start the server, drive it with the C load generator at each offered
     rate in turn, stop it; one result dict per rate."""
     soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
@@ -106,7 +120,7 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
     n_feat = 28
     tmp = tempfile.mkdtemp()
     bodies = os.path.join(tmp, "bodies.bin")
-    write_bodies(bodies, n_feat, 8, seed=3)
+    write_bodies(bodies, n_feat, 8, seed=3, protocol=protocol)
     env = dict(os.environ if env is None else env)
     if model == "c2":
         write_c2_model(tmp)
@@ -125,20 +139,22 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
         if not wait_ready(port, ready_timeout):
             raise RuntimeError("server did not become ready: " +
                                open(os.path.join(tmp, "server.log")).read()[-2000:])
-        warm(port, n_feat)
+        warm(port, n_feat, protocol=protocol)
         for q in qps_list:
             out = subprocess.run([LOADGEN, "--port", str(port), "--conns", str(conns),
                                   "--qps", str(q), "--duration", str(duration),
                                   "--warmup", str(warmup), "--bodies", bodies,
                                   "--threads", str(loadgen_threads),
-                                  "--path", "/v1/models/model:predict"],
+                                  "--path", predict_path(protocol)],
                                  capture_output=True, text=True,
                                  timeout=duration + warmup + 60)   # loadgen drains by +30 s
             if out.returncode != 0:
                 raise RuntimeError(f"loadgen failed: {out.stderr[-2000:]}")
             res = json.loads(out.stdout)
-            res.update({"config": "C5 dynamic batching: v1 :predict over HTTP, KFServer "
-                                  "in-process batcher", "model": model,
+            res.update({"config": ("C5 dynamic batching: V2 /infer FP32 JSON tensors" if
+                                   protocol == "v2" else "C5 dynamic batching: v1 :predict") +
+                                  " over HTTP, KFServer in-process batcher", "model": model,
+                        "protocol": protocol,
                         "workers": workers, "max_batch_size": max_batch,
                         "max_latency_ms": max_latency_ms,
                         "native_http": env.get("KF_NATIVE_HTTP", "1") != "0",
@@ -177,10 +193,13 @@ def main():
     p.add_argument("--io-threads", type=int, default=2,
                    help="native HTTP front end IO threads per worker (KF_NATIVE_HTTP=0: "
                         "the asyncio server)")
+    p.add_argument("--protocol", default="v1", choices=["v1", "v2"],
+                   help="v1 :predict instances, or V2 /infer FP32 JSON tensors")
     args = p.parse_args()
     serve_and_measure([float(x) for x in args.qps.split(",")], args.workers, args.io_threads,
                       args.duration, args.warmup, args.conns, args.port, args.model,
-                      args.max_batch, args.max_latency_ms, loadgen_threads=args.loadgen_threads)
+                      args.max_batch, args.max_latency_ms, loadgen_threads=args.loadgen_threads,
+                      protocol=args.protocol)
 
 
 if __name__ == "__main__":

@@ -82,7 +82,8 @@ def test_kfserve_library_exports_its_header():
     from kfserving_amd.kfserving import fastjson
     src = open(os.path.join(ROOT, "include", "kfserve.h")).read()
     names = sorted(set(re.findall(r"^\s*int\s+(kf_\w+)\(", src, re.M)))
-    assert names == ["kf_parse_inputs", "kf_parse_instances", "kf_parse_instances_mt"]
+    assert names == ["kf_parse_inputs", "kf_parse_instances", "kf_parse_instances_mt",
+                     "kf_parse_v2_tensor"]
     lib = fastjson.load_library()
     for n in names:
         assert hasattr(lib, n), n

@@ -114,3 +114,59 @@ def test_native_http_c2_large_bodies(tmp_path):
     finally:
         nat.stop()
         py.stop()
+
+
+def test_native_http_c2_v2_tensors(tmp_path):
+    """V2 tensor requests (FP32 / FP64 JSON data) on the C2 forest: after the
+    first (which makes the model's tensor batcher), each is answered on the
+    native route; the bytes equal the asyncio server's and the probabilities
+    are the oracle's (the float32 rows as DMatrix(ndarray) holds them)."""
+    import bench_serving as bs
+    from kfserving_amd.xgbserver import XGBoostModel
+    from oracle import xgb_ref
+    bs.write_c2_model(str(tmp_path))
+    runs = []
+    for native in (True, False):
+        m = XGBoostModel("model", str(tmp_path), 1)
+        assert m.load()
+        srv = KFServer(max_batchsize=65536, max_latency_ms=3)
+        srv.native_http = native
+        srv.register_model(m)
+        runs.append(_Running(srv))
+    nat, py = runs
+    t0 = time.time()
+    while nat.server.front_end is None and time.time() - t0 < 60:
+        time.sleep(0.05)
+    ref = xgb_ref.read_xgb_binary(os.path.join(str(tmp_path), "model.bst"))
+    rng = np.random.default_rng(12)
+    path = "/v2/models/model/infer"
+    try:
+        first = bs.body_of(rng.standard_normal((3, 28)).astype(np.float32), "v2")
+        assert nat.fetch(path, "POST", first)[0] == 200
+        fe = nat.server.front_end
+        assert "v2:model" in fe.routes
+        before = fe.stats()
+        for i in range(16):
+            rows = int(rng.integers(1, 65))
+            X = rng.standard_normal((rows, 28))
+            X[rng.random(X.shape) < 0.03] = np.nan
+            dt = "FP32" if i % 2 == 0 else "FP64"
+            req = {"inputs": [{"name": "x", "shape": [rows, 28], "datatype": dt,
+                               "data": X.reshape(-1).tolist() if i % 4 < 2 else X.tolist()}]}
+            if i % 3 == 0:
+                req["id"] = f"r{i}"
+            body = json.dumps(req).encode()
+            a = nat.fetch(path, "POST", body)
+            b = py.fetch(path, "POST", body)
+            assert a[0] == b[0] == 200 and a[1] == b[1] and a[2] == b[2]
+            out = json.loads(a[2])["outputs"][0]
+            assert out["datatype"] == "FP32" and out["shape"] == [rows]
+            np.testing.assert_allclose(np.asarray(out["data"]),
+                                       xgb_ref.predict(ref, X.astype(np.float32)), rtol=1e-5,
+                                       atol=0)
+        st = fe.stats()
+        assert st["native_requests"] - before["native_requests"] == 16
+        assert st["python_requests"] == before["python_requests"]
+    finally:
+        nat.stop()
+        py.stop()

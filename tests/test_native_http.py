@@ -478,3 +478,67 @@ def test_large_bodies_take_the_native_route(golden, tmp_path):
     finally:
         nat.stop()
         py.stop()
+
+
+def test_v2_tensor_route_bytes_equal_python_server(golden, tmp_path):
+    """V2 tensor requests (/v2/models/<name>/infer, JSON data) of xgbserver
+    take the native route once the application has made the model's tensor
+    batcher: FP32 / FP64, flat or row-nested data, a [F] tensor as one row,
+    an id echoed, JSON's NaN / Infinity and integers; every other V2 request
+    (outputs, parameters, other datatypes, ragged data, a size or width that
+    does not match, an escaped id) is the application's.  Bytes equal the
+    asyncio server's throughout."""
+    nat, py = _servers(golden, tmp_path)
+    rng = np.random.default_rng(9)
+    X = rng.uniform(0, 7, (6, 4)).round(3)
+
+    def t(data, shape, dt="FP32", **extra):
+        body = {"inputs": [{"name": "x", "shape": shape, "datatype": dt, "data": data}]}
+        body.update(extra)
+        return json.dumps(body).encode()
+    native = [
+        t(X.reshape(-1).tolist(), [6, 4]),
+        t(X.tolist(), [6, 4], "FP64", id="req-17"),
+        t(X[0].tolist(), [4]),
+        t([[1, 2.5, 0, 3], [4, 5, 6, 7]], [2, 4], "FP64"),
+        b'{"id": "q", "inputs": [{"data": [NaN, 1.0, Infinity, -Infinity], "datatype": "FP32",'
+        b' "shape": [1, 4], "name": "in"}]}',
+        t((X * 1e30).reshape(-1).tolist(), [6, 4], "FP32"),       # float32 overflow: inf
+    ]
+    fallback = [
+        t(X.reshape(-1).tolist(), [6, 4], outputs=[{"name": "predict"}]),
+        t(X.reshape(-1).tolist(), [6, 4], parameters={"binary_data_output": True}),
+        t([1, 2, 3, 4], [1, 4], "INT32"),
+        t([[1, 2, 3, 4], [5, 6, 7]], [2, 4]),
+        t(X.reshape(-1).tolist(), [5, 4]),
+        t(X[:, :3].reshape(-1).tolist(), [6, 3]),
+        t(X[0].tolist(), [4], id="été"),
+        t([], [0, 4]),
+        b'{"inputs": [{"name": "x", "shape": [1, 4], "datatype": "FP32", "data": [1, 2, 3, 4]},'
+        b' {"name": "y", "shape": [1, 4], "datatype": "FP32", "data": [1, 2, 3, 4]}]}',
+    ]
+    path = "/v2/models/xgboost-iris/infer"
+    try:
+        fe = nat.server.front_end
+        # the first tensor request makes the tensor batcher: the route follows
+        for body in [native[0]] + native + fallback:
+            a = nat.fetch(path, "POST", body)
+            b = py.fetch(path, "POST", body)
+            assert (a[0], dict(a[1].items())) == (b[0], dict(b[1].items())), (body[:90], a, b)
+            assert a[2] == b[2], (body[:90], a[2][:300], b[2][:300])
+        assert "v2:xgboost-iris" in fe.routes
+        st = fe.stats()
+        assert st["python_requests"] == 1 + len(fallback), st
+        assert st["native_requests"] == len(native), st
+        # binary tensor data stays with the application
+        raw = np.asarray(X, dtype=np.float32).tobytes()
+        head = json.dumps({"inputs": [{"name": "x", "shape": [6, 4], "datatype": "FP32",
+                                       "parameters": {"binary_data_size": len(raw)}}]}).encode()
+        hdr = {"Inference-Header-Content-Length": str(len(head))}
+        a = nat.fetch(path, "POST", head + raw, hdr)
+        b = py.fetch(path, "POST", head + raw, hdr)
+        assert (a[0], dict(a[1].items()), a[2]) == (b[0], dict(b[1].items()), b[2])
+        assert fe.stats()["python_requests"] == 2 + len(fallback)
+    finally:
+        nat.stop()
+        py.stop()
