@@ -97,7 +97,8 @@ int kh_add_v1_inputs_predict(void* srv, const char* model, void* batcher, int32_
 /* Answer V2 tensor requests on POST /v2/models/<model>/infer natively through
  * `batcher` (the model's batcher of V2 tensor rows): a body kf_parse_v2_tensor
  * takes, of n_cols columns, is converted to the batcher's type as numpy casts
- * it (FP32 data rounded to float32 first) and answered as
+ * it (FP32 data rounded to float32 first; `transform` as kh_add_v1_predict's:
+ * KB_IN_PLAIN and KH_CHECK_* flags) and answered as
  * kfserving_amd/kfserving/v2.py encode_response answers it:
  * {"model_name": ..., ["id": ...,] "outputs": [{"name": "predict", "shape":
  * [N] or [N, out_width], "datatype": "FP32" | "FP64", "data": [...]}]}.
@@ -105,7 +106,7 @@ int kh_add_v1_inputs_predict(void* srv, const char* model, void* batcher, int32_
  * goes to the application.  The route is removed with
  * kh_remove_route(srv, "v2:<model>"). */
 int kh_add_v2_tensor_predict(void* srv, const char* model, void* batcher, int32_t n_cols,
-                             int32_t out_width, int32_t out_elem_bytes);
+                             int32_t out_width, int32_t out_elem_bytes, int32_t transform);
 
 /* Stop answering the model natively (its requests go to the application):
  * the batcher's forming batch is flushed, the requests already submitted are

@@ -1099,8 +1099,9 @@ int kh_add_v1_inputs_predict(void* h, const char* model, void* batcher, int32_t 
 }
 
 int kh_add_v2_tensor_predict(void* h, const char* model, void* batcher, int32_t n_cols,
-                             int32_t out_width, int32_t out_elem_bytes) {
-  return add_route(h, model, batcher, n_cols, out_width, out_elem_bytes, KB_IN_PLAIN, nullptr,
+                             int32_t out_width, int32_t out_elem_bytes, int32_t transform) {
+  if ((transform & 0xFF) != KB_IN_PLAIN) return -1;   // numpy's cast, nothing else
+  return add_route(h, model, batcher, n_cols, out_width, out_elem_bytes, transform, nullptr,
                    nullptr, 0, nullptr, nullptr, true);
 }
 

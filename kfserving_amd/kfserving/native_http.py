@@ -73,7 +73,7 @@ def load_library() -> ctypes.CDLL:
     lib.kh_add_v1_inputs_predict.argtypes = [vp, ctypes.c_char_p, vp, i32, i32, i32,
                                              ctypes.c_char_p, ctypes.POINTER(i32)]
     lib.kh_add_v2_tensor_predict.restype = ctypes.c_int
-    lib.kh_add_v2_tensor_predict.argtypes = [vp, ctypes.c_char_p, vp, i32, i32, i32]
+    lib.kh_add_v2_tensor_predict.argtypes = [vp, ctypes.c_char_p, vp, i32, i32, i32, i32]
     lib.kh_remove_route.restype = ctypes.c_int
     lib.kh_remove_route.argtypes = [vp, ctypes.c_char_p]
     lib.kh_start.restype = ctypes.c_int
@@ -226,23 +226,25 @@ class NativeFrontEnd:
 
     def _on_tensor_batcher(self, event: str, name: str, batcher) -> None:
         """V2 tensor requests (/v2/models/<name>/infer with "datatype") of a
-        plugin that declares ``native_v2_tensor`` go natively through the
-        model's tensor batcher, which the application makes on the first
-        such request (route key "v2:<name>")."""
+        plugin that declares ``native_v2_transform`` (its tensor conversion
+        as kb_submit_convert's plain cast plus KH_CHECK_* flags) go natively
+        through the model's tensor batcher, which the application makes on
+        the first such request (route key "v2:<name>")."""
         key = "v2:" + name
         if event == "retire" and key in self.routes:
             self._lib.kh_remove_route(self._h, key.encode())
             del self.routes[key]
         elif event == "create" and key not in self.routes:
             model = batcher.model
-            if not getattr(model, "native_v2_tensor", False) or \
-                    not route_spec_static(self.app, model):
+            tr = getattr(model, "native_v2_transform", None)
+            if tr is None or not route_spec_static(self.app, model):
                 return
             spec = _spec_of(batcher, model)
             if spec is None:
                 return
             h, F, w, e = spec[:4]
-            if self._lib.kh_add_v2_tensor_predict(self._h, name.encode(), h, F, w, e) == 0:
+            if self._lib.kh_add_v2_tensor_predict(self._h, name.encode(), h, F, w, e,
+                                                  int(tr)) == 0:
                 self.routes[key] = h
 
     def stats(self) -> dict:

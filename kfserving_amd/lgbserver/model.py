@@ -67,6 +67,10 @@ class LightGBMModel(GPUForestMixin, KFModel):
     def native_v1_names(self):
         return self.feature_name()
 
+    # V2 tensors: tensor_matrix reads the columns in the booster's order as
+    # float64 (FP32 data widened exactly), the plain cast of the native route
+    native_v2_transform = 0
+
     # KFServer's in-process batcher (kfserving_amd.batcher.ModelBatcher, kind
     # "inputs"): one request's rows as the float64 matrix its columns select,
     # then one predict over the concatenated rows of a batch

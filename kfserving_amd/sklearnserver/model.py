@@ -93,6 +93,17 @@ class SKLearnModel(GPUForestMixin, KFModel):  # pylint:disable=c-extension-no-me
             return None
         return (1 << 8) | (0 if f.meta.get("allow_nan", True) else (1 << 9))
 
+    @property
+    def native_v2_transform(self):
+        """V2 tensors take request_matrix's checks and float32 cast too
+        (native_rows), so regressors answer them natively with the same flags;
+        a classifier's labels come back as a typed tensor, which the
+        application encodes."""
+        f = self._forest
+        if f is None or f.meta.get("classes") is not None:
+            return None
+        return self.native_v1_transform
+
     def native_v1_labels(self):
         """A classifier's labels as its predict renders them
         (classes.take(index).tolist() -> json.dumps), for the native route."""

@@ -56,7 +56,7 @@ class XGBoostModel(GPUForestMixin, KFModel):
     native_v1_transform = 1
     # ... and its V2 tensor requests (FP32 / FP64 JSON data, kh_add_v2_tensor_predict):
     # tensor_matrix is the plain float32 cast the native batcher applies
-    native_v2_tensor = True
+    native_v2_transform = 0
 
     def native_request(self, chunk, kind: str):
         # a natively decoded JSON list: DMatrix(list)'s rule (0 missing, NaN

@@ -542,3 +542,88 @@ def test_v2_tensor_route_bytes_equal_python_server(golden, tmp_path):
     finally:
         nat.stop()
         py.stop()
+
+
+def _v2(data, shape, dt="FP64", **extra):
+    body = {"inputs": [{"name": "x", "shape": shape, "datatype": dt, "data": data}]}
+    body.update(extra)
+    return json.dumps(body).encode()
+
+
+def _v2_pairs(nat, py, path, bodies):
+    for body in bodies:
+        a = nat.fetch(path, "POST", body)
+        b = py.fetch(path, "POST", body)
+        assert (a[0], dict(a[1].items()), a[2]) == (b[0], dict(b[1].items()), b[2]), \
+            (body[:90], a, b)
+
+
+def test_v2_tensor_route_lgbserver_and_sklearn_regressor(golden, tmp_path):
+    """The V2 tensor route of lgbserver (float64 columns in booster order,
+    FP64 output) and of a sklearn regressor (the float32 cast with its
+    checks: a value beyond float32 or a NaN it rejects goes to the
+    application), byte for byte as the asyncio server."""
+    from tests.test_lgb_batching import _lgb_model
+    from kfserving_amd.sklearnserver import SKLearnModel
+    # lgbserver
+    runs = []
+    for native in (True, False):
+        srv = KFServer(max_batchsize=64, max_latency_ms=3)
+        srv.native_http = native
+        (tmp_path / ("ln" if native else "lp")).mkdir()
+        srv.register_model(_lgb_model(golden, tmp_path / ("ln" if native else "lp")))
+        runs.append(_Running(srv))
+    nat, py = runs
+    _wait_front_end(nat)
+    name = nat.server.front_end.app.models.get_models()[0].name
+    path = f"/v2/models/{name}/infer"
+    rng = np.random.default_rng(3)
+    X = rng.uniform(0, 7, (5, 4)).round(2)
+    try:
+        _v2_pairs(nat, py, path, [_v2(X.tolist(), [5, 4])])     # makes the tensor batcher
+        before = nat.server.front_end.stats()
+        _v2_pairs(nat, py, path, [_v2(X.reshape(-1).tolist(), [5, 4]),
+                                  _v2(X[1].tolist(), [4], "FP32", id="a"),
+                                  _v2([[float("nan"), 1, 2, 3]], [1, 4], "FP64")])
+        st = nat.server.front_end.stats()
+        assert st["native_requests"] - before["native_requests"] == 3
+        assert f"v2:{name}" in nat.server.front_end.routes
+    finally:
+        nat.stop()
+        py.stop()
+    # a sklearn regressor without missing-value support
+    g = np.load(os.path.join(golden, "sk_rf_reg.npz"))
+    Xs = np.nan_to_num(g["X"][:4]).astype(np.float64)
+    F = Xs.shape[1]
+    runs = []
+    for native in (True, False):
+        d = tmp_path / f"sk{native}"
+        d.mkdir()
+        shutil.copy(os.path.join(golden, "sk_rf_reg_model.npz"), str(d / "model.npz"))
+        m = SKLearnModel("sk", str(d))
+        assert m.load()
+        m._forest.meta["allow_nan"] = False
+        m.predict_matrix = lambda X, kind=OUT_PREDICT, m=m: canon_eval.predict(m._forest, X, kind)
+        srv = KFServer(max_batchsize=64, max_latency_ms=3)
+        srv.native_http = native
+        srv.register_model(m)
+        runs.append(_Running(srv))
+    nat, py = runs
+    _wait_front_end(nat)
+    path = "/v2/models/sk/infer"
+    bad = Xs[:2].copy()
+    bad[1, 0] = 1e39
+    try:
+        _v2_pairs(nat, py, path, [_v2(Xs.tolist(), [4, F])])
+        before = nat.server.front_end.stats()
+        _v2_pairs(nat, py, path, [_v2(Xs.reshape(-1).tolist(), [4, F], "FP32"),
+                                  _v2(Xs[0].tolist(), [F], id="one")])
+        mid = nat.server.front_end.stats()
+        assert mid["native_requests"] - before["native_requests"] == 2
+        _v2_pairs(nat, py, path, [_v2(bad.tolist(), [2, F]),                       # > float32
+                                  _v2([[float("nan")] + [0.5] * (F - 1)], [1, F])])  # NaN
+        st = nat.server.front_end.stats()
+        assert st["python_requests"] - mid["python_requests"] == 2
+    finally:
+        nat.stop()
+        py.stop()
