@@ -69,20 +69,25 @@ int kf_parse_inputs(const char* body, int64_t len, const char* names,
                     int64_t* rows);
 
 /* A V2 inference request body (POST /v2/models/<name>/infer; the V2 protocol's
- * JSON tensor form, docs/predict-api/v2/required_api.md:205-225) with one
- * FP32 or FP64 input of shape [F] (one row) or [N, F], its "data" flat or one
- * level of equal-length rows, as the float64 values numpy reads
- * (v2.decode_inputs: np.asarray(data, dtype).reshape(shape); a [F] tensor is
- * one row).  The request may carry an "id" (echoed in the response);
- * *id_off / *id_len give its JSON text, quotes included (0 / 0 when absent).
- * KF_FALLBACK for everything else -- other keys ("outputs", "parameters",
- * binary data), other datatypes, more tensors, strings with escapes or
- * non-ASCII, ragged or deeper data, a size that is not the shape's -- which
- * the application decodes (kfserving_amd/kfserving/v2.py).  *datatype: 0
- * FP32, 1 FP64.  KF_ERR_SPACE: out holds fewer than *rows * *cols values. */
-int kf_parse_v2_tensor(const char* body, int64_t len, double* out, int64_t cap,
-                       int64_t* rows, int64_t* cols, int32_t* datatype,
-                       int64_t* id_off, int64_t* id_len);
+ * tensor form, docs/predict-api/v2/required_api.md:205-225) with one FP32 or
+ * FP64 input of shape [F] (one row) or [N, F], as the float64 values numpy
+ * reads (v2.decode_inputs: np.asarray(data, dtype).reshape(shape), or
+ * np.frombuffer of the binary tensor data; a [F] tensor is one row).
+ * head_len < 0: the whole body is the JSON request; else body[0, head_len) is
+ * it (the Inference-Header-Content-Length header) and body[head_len, len) the
+ * binary tensor data, which the input claims whole with "parameters":
+ * {"binary_data_size": n}.  The input's "data" is flat or one level of
+ * equal-length rows.  The request may carry an "id" (*id_off / *id_len give
+ * its JSON text, quotes included; 0 / 0 when absent) and "parameters":
+ * {"binary_data_output": bool} (*binary_output).  KF_FALLBACK for everything
+ * else -- "outputs", other parameters, other datatypes, more tensors, strings
+ * with escapes or non-ASCII, ragged or deeper data, a size that is not the
+ * shape's, binary data no input claims -- which the application decodes
+ * (kfserving_amd/kfserving/v2.py).  *datatype: 0 FP32, 1 FP64.
+ * KF_ERR_SPACE: out holds fewer than *rows * *cols values. */
+int kf_parse_v2_tensor(const char* body, int64_t len, int64_t head_len, double* out,
+                       int64_t cap, int64_t* rows, int64_t* cols, int32_t* datatype,
+                       int64_t* id_off, int64_t* id_len, int32_t* binary_output);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -85,6 +85,7 @@ struct Conn {
   int64_t rows = 0;
   bool keep = true;
   std::string model, v2_id;   // a V2 tensor answer: the model's name, the request's id text
+  bool v2_binary = false;     // ... asked as binary tensor data (binary_data_output)
   // the request handed to Python (kept until kh_respond)
   std::string method, target, version, headers, body;
 };
@@ -284,13 +285,14 @@ void append_json_string(std::string& o, const std::string& s) {
 // kfserver._serialize: status line, the handler's headers, Content-Length,
 // Server, and Connection: close when the connection ends
 void append_response(std::string& o, int code, const char* reason, const char* ctype,
-                     const std::string& body, bool keep) {
+                     const std::string& body, bool keep, const std::string& extra = std::string()) {
   o += "HTTP/1.1 ";
   o += std::to_string(code);
   o += ' ';
   o += reason;
   o += "\r\nContent-Type: ";
   o += ctype;
+  o += extra;   // the handler's further headers, "\r\nName: value" each
   o += "\r\nContent-Length: ";
   o += std::to_string(body.size());
   o += "\r\nServer: kfserving-amd\r\n";
@@ -558,8 +560,19 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   // /v2/.../infer answers a v1 body as :predict does (ref kfserver.py:77-78);
   // a V2 tensor request (a "datatype" in the body) takes the model's V2
   // route if it has one, and binary tensor data is the application's
-  if (v2 && r.h.count("inference-header-content-length")) return false;
-  const bool tensor = v2 && r.body.find("\"datatype\"") != std::string::npos;
+  int64_t head_len = -1;   // the binary tensor extension: the JSON part's bytes
+  if (v2) {
+    auto ih = r.h.find("inference-header-content-length");
+    if (ih != r.h.end()) {
+      const std::string& t = ih->second;
+      if (t.empty() || t.size() > 12 ||
+          !std::all_of(t.begin(), t.end(), [](char ch) { return ch >= '0' && ch <= '9'; }))
+        return false;   // the application's int() decides
+      head_len = std::stoll(t);
+      if (head_len > static_cast<int64_t>(r.body.size())) return false;   // its 400
+    }
+  }
+  const bool tensor = v2 && (head_len >= 0 || r.body.find("\"datatype\"") != std::string::npos);
   Route route;
   {
     // the reservation is taken under the route lock: kh_remove_route erases
@@ -602,11 +615,12 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   int64_t rows = 0, cols = 0;
   int32_t x_dtype = 1;   // the rows handed to the batcher: float64 (0: float32)
   int64_t id_off = 0, id_len = 0;
+  int32_t bin_out = 0;
   if (tensor) {   // {"inputs": [{"name", "shape", "datatype", "data"}], "id"}
     int32_t dt = -1;
-    if (kf_parse_v2_tensor(r.body.data(), static_cast<int64_t>(r.body.size()), xb,
-                           static_cast<int64_t>(xb_n), &rows, &cols, &dt, &id_off,
-                           &id_len) != KF_PARSED ||
+    if (kf_parse_v2_tensor(r.body.data(), static_cast<int64_t>(r.body.size()), head_len, xb,
+                           static_cast<int64_t>(xb_n), &rows, &cols, &dt, &id_off, &id_len,
+                           &bin_out) != KF_PARSED ||
         cols != route.n_cols)
       return false;   // the application: v2.decode_inputs, or an unbatched predict
     if (dt == 0) {    // np.asarray(data, float32): each value rounded to float32
@@ -651,6 +665,7 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
   if (tensor) {
     c->model = name;
     c->v2_id.assign(r.body, static_cast<size_t>(id_off), static_cast<size_t>(id_len));
+    c->v2_binary = bin_out != 0;
   }
   c->res.assign(static_cast<size_t>(rows) * route.out_width * route.out_elem, 0);
   c->busy = true;
@@ -696,8 +711,24 @@ void answer_v2(Conn* c, const kb_completion& d, const std::string& err) {
       body += ", ";
       body += std::to_string(w);
     }
-    body += c->route.out_elem == 4 ? "], \"datatype\": \"FP32\", \"data\": [" : "], \"datatype\": \"FP64\", \"data\": [";
+    body += c->route.out_elem == 4 ? "], \"datatype\": \"FP32\"" : "], \"datatype\": \"FP64\"";
     const size_t n = static_cast<size_t>(c->rows) * w;
+    if (c->v2_binary) {   // the binary tensor extension: JSON head, then the raw output
+      const size_t raw = n * static_cast<size_t>(c->route.out_elem);
+      body += ", \"parameters\": {\"binary_data_size\": ";
+      body += std::to_string(raw);
+      body += "}}]}";
+      const std::string extra = "\r\nInference-Header-Content-Length: " + std::to_string(body.size());
+      body.append(reinterpret_cast<const char*>(c->res.data()), raw);   // little endian
+      append_response(c->out, 200, "OK", "application/octet-stream", body, c->keep, extra);
+      c->close_after = c->close_after || !c->keep;
+      std::vector<unsigned char>().swap(c->res);
+      c->model.clear();
+      c->v2_id.clear();
+      c->v2_binary = false;
+      return;
+    }
+    body += ", \"data\": [";
     for (size_t i = 0; i < n; ++i) {
       if (i) body += ", ";
       double v;
@@ -717,6 +748,7 @@ void answer_v2(Conn* c, const kb_completion& d, const std::string& err) {
   std::vector<unsigned char>().swap(c->res);
   c->model.clear();
   c->v2_id.clear();
+  c->v2_binary = false;
 }
 
 void answer_native(Conn* c, const kb_completion& d, const std::string& err) {

@@ -689,21 +689,46 @@ bool tensor_data(Scanner& sc, double* out, int64_t cap, int64_t* n) {
   return true;
 }
 
+
+// {"key": <value>} with one key: a non-negative int ("binary_data_size") or
+// a boolean ("binary_data_output"); anything else is the application's
+bool one_key_object(Scanner& sc, const char* key, size_t key_len, bool boolean, int64_t* v) {
+  if (!sc.eat('{')) return false;
+  sc.ws();
+  if (!sc.lit(key, key_len)) return false;
+  sc.ws();
+  if (!sc.eat(':')) return false;
+  sc.ws();
+  if (boolean) {
+    if (sc.lit("true", 4)) *v = 1;
+    else if (sc.lit("false", 5)) *v = 0;
+    else return false;
+  } else if (!shape_int(sc, v)) {
+    return false;
+  }
+  sc.ws();
+  return sc.eat('}');
+}
+
 }  // namespace
 
-extern "C" int kf_parse_v2_tensor(const char* body, int64_t len, double* out, int64_t cap,
-                                  int64_t* rows, int64_t* cols, int32_t* datatype,
-                                  int64_t* id_off, int64_t* id_len) {
-  if (!body || len < 0 || !rows || !cols || !datatype || !id_off || !id_len) return KF_FALLBACK;
+extern "C" int kf_parse_v2_tensor(const char* body, int64_t len, int64_t head_len, double* out,
+                                  int64_t cap, int64_t* rows, int64_t* cols, int32_t* datatype,
+                                  int64_t* id_off, int64_t* id_len, int32_t* binary_output) {
+  if (!body || len < 0 || head_len > len || !rows || !cols || !datatype || !id_off || !id_len ||
+      !binary_output)
+    return KF_FALLBACK;
   *rows = *cols = 0;
   *datatype = -1;
   *id_off = *id_len = 0;
-  Scanner sc{body, body + len};
-  bool seen_inputs = false, seen_id = false, overflow = false;
-  int64_t shape[2] = {0, 0}, ndim = -1, count = -1;
+  *binary_output = 0;
+  const int64_t hl = head_len < 0 ? len : head_len;
+  Scanner sc{body, body + hl};
+  bool seen_inputs = false, seen_id = false, seen_params = false, overflow = false;
+  int64_t shape[2] = {0, 0}, ndim = -1, count = -1, bsize = -1;
   sc.ws();
   if (!sc.eat('{')) return KF_FALLBACK;
-  for (;;) {   // the request's keys: "inputs" and "id" only
+  for (;;) {   // the request's keys: "inputs", "id" and "parameters" only
     sc.ws();
     if (sc.lit("\"inputs\"", 8)) {
       if (seen_inputs) return KF_FALLBACK;
@@ -714,7 +739,7 @@ extern "C" int kf_parse_v2_tensor(const char* body, int64_t len, double* out, in
       if (!sc.eat('[')) return KF_FALLBACK;
       sc.ws();
       if (!sc.eat('{')) return KF_FALLBACK;   // exactly one tensor
-      bool s_name = false, s_shape = false, s_type = false, s_data = false;
+      bool s_name = false, s_shape = false, s_type = false, s_data = false, s_par = false;
       for (;;) {
         sc.ws();
         if (sc.lit("\"name\"", 6)) {
@@ -761,15 +786,23 @@ extern "C" int kf_parse_v2_tensor(const char* body, int64_t len, double* out, in
           sc.ws();
           if (!tensor_data(sc, out, cap, &count)) return KF_FALLBACK;
           if (count > cap) overflow = true;
+        } else if (sc.lit("\"parameters\"", 12)) {   // binary tensor data
+          if (s_par) return KF_FALLBACK;
+          s_par = true;
+          sc.ws();
+          if (!sc.eat(':')) return KF_FALLBACK;
+          sc.ws();
+          if (!one_key_object(sc, "\"binary_data_size\"", 18, false, &bsize)) return KF_FALLBACK;
         } else {
-          return KF_FALLBACK;   // "parameters" (binary data) and the rest: the application
+          return KF_FALLBACK;
         }
         sc.ws();
         if (sc.eat(',')) continue;
         if (sc.eat('}')) break;
         return KF_FALLBACK;
       }
-      if (!(s_shape && s_type && s_data)) return KF_FALLBACK;
+      // JSON data or binary data, not both
+      if (!(s_shape && s_type && (s_data != (bsize >= 0)))) return KF_FALLBACK;
       sc.ws();
       if (!sc.eat(']')) return KF_FALLBACK;   // a second tensor: the application
     } else if (sc.lit("\"id\"", 4)) {
@@ -783,8 +816,17 @@ extern "C" int kf_parse_v2_tensor(const char* body, int64_t len, double* out, in
       if (!plain_string(sc, &s, &n)) return KF_FALLBACK;
       *id_off = s - body;
       *id_len = n;
+    } else if (sc.lit("\"parameters\"", 12)) {   // {"binary_data_output": bool}
+      if (seen_params) return KF_FALLBACK;
+      seen_params = true;
+      sc.ws();
+      if (!sc.eat(':')) return KF_FALLBACK;
+      sc.ws();
+      int64_t b = 0;
+      if (!one_key_object(sc, "\"binary_data_output\"", 20, true, &b)) return KF_FALLBACK;
+      *binary_output = static_cast<int32_t>(b);
     } else {
-      return KF_FALLBACK;   // "outputs", "parameters", ...: the application
+      return KF_FALLBACK;   // "outputs" and the rest: the application
     }
     sc.ws();
     if (sc.eat(',')) continue;
@@ -792,11 +834,34 @@ extern "C" int kf_parse_v2_tensor(const char* body, int64_t len, double* out, in
     return KF_FALLBACK;
   }
   sc.ws();
-  if (sc.p != sc.end || !seen_inputs) return KF_FALLBACK;
+  if (sc.p != sc.end || !seen_inputs || ndim < 1) return KF_FALLBACK;
   // np.asarray(data).size == prod(shape), reshaped; a [F] tensor is one row
   const int64_t r = ndim == 1 ? 1 : shape[0];
   const int64_t c = ndim == 1 ? shape[0] : shape[1];
-  if (ndim < 1 || r <= 0 || c <= 0 || r * c != count) return KF_FALLBACK;
+  if (r <= 0 || c <= 0) return KF_FALLBACK;
+  const int64_t tail = len - hl;
+  if (bsize >= 0) {   // np.frombuffer of the tail: little-endian FP32 / FP64
+    const int64_t es = *datatype == 0 ? 4 : 8;
+    if (bsize != r * c * es || bsize != tail) return KF_FALLBACK;   // every byte one input's
+    count = r * c;
+    if (count > cap) {
+      overflow = true;
+    } else {
+      const char* t = body + hl;
+      for (int64_t i = 0; i < count; ++i) {
+        if (es == 4) {
+          float f;
+          std::memcpy(&f, t + i * 4, 4);
+          out[i] = f;
+        } else {
+          std::memcpy(&out[i], t + i * 8, 8);
+        }
+      }
+    }
+  } else if (tail != 0) {
+    return KF_FALLBACK;   // binary data no input claims: the application's error
+  }
+  if (r * c != count) return KF_FALLBACK;
   *rows = r;
   *cols = c;
   return overflow ? KF_ERR_SPACE : KF_PARSED;

@@ -504,10 +504,12 @@ def test_v2_tensor_route_bytes_equal_python_server(golden, tmp_path):
         b'{"id": "q", "inputs": [{"data": [NaN, 1.0, Infinity, -Infinity], "datatype": "FP32",'
         b' "shape": [1, 4], "name": "in"}]}',
         t((X * 1e30).reshape(-1).tolist(), [6, 4], "FP32"),       # float32 overflow: inf
+        t(X.reshape(-1).tolist(), [6, 4], parameters={"binary_data_output": True}),
+        t(X.reshape(-1).tolist(), [6, 4], parameters={"binary_data_output": False}, id="b"),
     ]
     fallback = [
         t(X.reshape(-1).tolist(), [6, 4], outputs=[{"name": "predict"}]),
-        t(X.reshape(-1).tolist(), [6, 4], parameters={"binary_data_output": True}),
+        t(X.reshape(-1).tolist(), [6, 4], parameters={"binary_data_output": 1}),
         t([1, 2, 3, 4], [1, 4], "INT32"),
         t([[1, 2, 3, 4], [5, 6, 7]], [2, 4]),
         t(X.reshape(-1).tolist(), [5, 4]),
@@ -530,15 +532,32 @@ def test_v2_tensor_route_bytes_equal_python_server(golden, tmp_path):
         st = fe.stats()
         assert st["python_requests"] == 1 + len(fallback), st
         assert st["native_requests"] == len(native), st
-        # binary tensor data stays with the application
-        raw = np.asarray(X, dtype=np.float32).tobytes()
-        head = json.dumps({"inputs": [{"name": "x", "shape": [6, 4], "datatype": "FP32",
-                                       "parameters": {"binary_data_size": len(raw)}}]}).encode()
-        hdr = {"Inference-Header-Content-Length": str(len(head))}
-        a = nat.fetch(path, "POST", head + raw, hdr)
-        b = py.fetch(path, "POST", head + raw, hdr)
-        assert (a[0], dict(a[1].items()), a[2]) == (b[0], dict(b[1].items()), b[2])
-        assert fe.stats()["python_requests"] == 2 + len(fallback)
+        # the binary tensor extension (Inference-Header-Content-Length): input
+        # and output natively; a size that does not match, or bytes no input
+        # claims, are the application's
+        def binreq(Xb, dt, size=None, extra=b"", **top):
+            raw = Xb.astype(np.float32 if dt == "FP32" else np.float64).tobytes()
+            req = {"inputs": [{"name": "x", "shape": list(Xb.shape), "datatype": dt,
+                               "parameters": {"binary_data_size": size or len(raw)}}]}
+            req.update(top)
+            head = json.dumps(req).encode()
+            return head + raw + extra, {"Inference-Header-Content-Length": str(len(head))}
+        bin_native = [binreq(X, "FP32"), binreq(X, "FP64", id="k"),
+                      binreq(X[:2], "FP32", parameters={"binary_data_output": True}),
+                      (t(X.tolist(), [6, 4]), {"Inference-Header-Content-Length":
+                                               str(len(t(X.tolist(), [6, 4])))})]
+        bin_fallback = [binreq(X, "FP32", size=12), binreq(X, "FP32", extra=b"xx"),
+                        (t(X.tolist(), [6, 4]), {"Inference-Header-Content-Length": "abc"}),
+                        (t(X.tolist(), [6, 4]), {"Inference-Header-Content-Length": "99999"})]
+        n0 = fe.stats()
+        for body, hdr in bin_native + bin_fallback:
+            a = nat.fetch(path, "POST", body, hdr)
+            b = py.fetch(path, "POST", body, hdr)
+            assert (a[0], dict(a[1].items()), a[2]) == (b[0], dict(b[1].items()), b[2]), \
+                (body[:90], a[:2], b[:2])
+        n1 = fe.stats()
+        assert n1["native_requests"] - n0["native_requests"] == len(bin_native)
+        assert n1["python_requests"] - n0["python_requests"] == len(bin_fallback)
     finally:
         nat.stop()
         py.stop()
