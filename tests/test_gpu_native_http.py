@@ -167,6 +167,19 @@ def test_native_http_c2_v2_tensors(tmp_path):
         st = fe.stats()
         assert st["native_requests"] - before["native_requests"] == 16
         assert st["python_requests"] == before["python_requests"]
+        # the binary tensor extension, in and out
+        X = rng.standard_normal((40, 28)).astype(np.float32)
+        head = json.dumps({"inputs": [{"name": "x", "shape": [40, 28], "datatype": "FP32",
+                                       "parameters": {"binary_data_size": X.nbytes}}],
+                           "parameters": {"binary_data_output": True}}).encode()
+        hdr = {"Inference-Header-Content-Length": str(len(head))}
+        a = nat.fetch(path, "POST", head + X.tobytes(), hdr)
+        b = py.fetch(path, "POST", head + X.tobytes(), hdr)
+        assert a[0] == b[0] == 200 and a[1] == b[1] and a[2] == b[2]
+        n = int(a[1]["Inference-Header-Content-Length"])
+        got = np.frombuffer(a[2][n:], dtype="<f4")
+        np.testing.assert_allclose(got, xgb_ref.predict(ref, X), rtol=1e-5, atol=0)
+        assert fe.stats()["native_requests"] - st["native_requests"] == 1
     finally:
         nat.stop()
         py.stop()
