@@ -151,6 +151,9 @@ def parse_args(argv=None):
                    help="C5 over HTTP: offered req/s of the points (empty: skip); rank 0, "
                         "after the GPU legs, a server of one worker per GPU")
     p.add_argument("--c5-http-seconds", type=float, default=4.0)
+    p.add_argument("--c5-http-v2-qps", default="100000",
+                   help="the same with V2 FP32 JSON tensor bodies on /v2/models/<name>/infer "
+                        "(empty: skip)")
     p.add_argument("--no-tree-shard", action="store_true",
                    help="skip the tree-sharded C2 leg (every rank a slice of the trees, "
                         "partial margins summed by one reduce: RCCL over xGMI at N > 1)")
@@ -648,7 +651,7 @@ def native_batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_laten
             "_lat_ms": lat_ms}
 
 
-def c5_http_leg(args, world):
+def c5_http_leg(args, world, protocol="v1"):
     """BASELINE config C5 as named, over HTTP: xgbserver with the C2 forest
     (`python -m kfserving_amd.xgbserver`, --max_batchsize 65536
     --max_latency_ms 5) behind the native HTTP front end and native batcher,
@@ -667,13 +670,15 @@ def c5_http_leg(args, world):
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
               "MASTER_PORT", "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
-    qps = [float(q) for q in args.c5_http_qps.split(",") if q.strip()]
+    spec = args.c5_http_v2_qps if protocol == "v2" else args.c5_http_qps
+    qps = [float(q) for q in spec.split(",") if q.strip()]
     io = max(2, 16 // world)
     try:
         pts = bs.serve_and_measure(qps, workers=world, io_threads=io,
                                    duration=args.c5_http_seconds, warmup=1.5, conns=4096,
-                                   port=18090 + (os.getpid() % 500), env=env,
-                                   ready_timeout=90, loadgen_threads=4, echo=False)
+                                   port=18090 + (os.getpid() % 500) + (600 if protocol == "v2" else 0),
+                                   env=env, ready_timeout=90, loadgen_threads=4, echo=False,
+                                   protocol=protocol)
     except Exception as e:   # reported, not fatal: the headline stands without it
         return {"error": str(e)[-500:]}
     keep = ("offered_qps", "req_per_s", "rows_per_s", "p50_ms", "p90_ms", "p99_ms", "max_ms",
@@ -684,6 +689,8 @@ def c5_http_leg(args, world):
             "max_latency_ms": 5, "model": "C2 (500 x depth 8, 28 features), xgbserver",
             "path": "HTTP/1.1 keep-alive -> native front end (kfhttp.h) -> native batcher "
                     "(kfbatch.h) -> ti_predict (host buffers)",
+            "protocol": ("V2 /infer, one FP32 tensor of JSON data" if protocol == "v2"
+                         else "v1 :predict instances"),
             "points": [{k: p.get(k) for k in keep} for p in pts]}
 
 
@@ -1214,9 +1221,11 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
         dist.destroy_process_group()
     if rank != 0:
         return None
-    c5_http = None
+    c5_http = c5_http_v2 = None
     if args.c5_http_qps and device != "cpu":
         c5_http = c5_http_leg(args, world)
+    if args.c5_http_v2_qps and device != "cpu":
+        c5_http_v2 = c5_http_leg(args, world, "v2")
     cpu = None
     if not args.no_cpu_baseline:
         cpu = cpu_baseline(trees, ti, X_host, args.cpu_seconds)
@@ -1266,6 +1275,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             "host_pipeline": host_pipeline,
             "tree_shard": tree_shard,
             "c5_http": c5_http,
+            "c5_http_v2": c5_http_v2,
         }
         line.update(configs)
     return line

@@ -30,7 +30,7 @@ def _rank(rank, port, q):
                                  "--configs", "c3", "--rows3", "200000", "--config-steps", "1",
                                  "--no-cpu-baseline", "--latency-qps", "0", "--host-rows", "0",
                                  "--nan-variant", "0", "--c5-http-qps", "5000",
-                                 "--c5-http-seconds", "2"])
+                                 "--c5-http-v2-qps", "5000", "--c5-http-seconds", "2"])
         q.put((rank, bench.run(args, device="cuda", backend="gloo"), None))
     except Exception as e:          # surface the failure in the parent
         q.put((rank, None, repr(e)))
@@ -68,3 +68,6 @@ def test_two_ranks_one_gpu_gloo():
     assert c5 is not None and "error" not in c5, c5
     assert c5["workers"] == 2 and c5["devices"] == 2
     assert all(p["lost"] == 0 and p["non200"] == 0 and p["requests"] > 0 for p in c5["points"])
+    c5v2 = line["c5_http_v2"]
+    assert c5v2 is not None and "error" not in c5v2 and c5v2["workers"] == 2, c5v2
+    assert all(p["lost"] == 0 and p["non200"] == 0 and p["requests"] > 0 for p in c5v2["points"])
