@@ -629,7 +629,6 @@ bool try_native(IoThread& t, Conn* c, Req& r, bool keep) {
       x_dtype = 0;
     }
   } else if (route.names) {   // lgbserver: {"inputs": [{column: [...]}, ...]}
-    if (r.body.size() >= KF_MT_MIN_BYTES) return false;   // the application's path
     const int32_t* offs = route.name_offsets->data();
     int rc = kf_parse_inputs(r.body.data(), static_cast<int64_t>(r.body.size()),
                              route.names->data(), offs, route.n_cols, xb,

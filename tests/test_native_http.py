@@ -646,3 +646,40 @@ def test_v2_tensor_route_lgbserver_and_sklearn_regressor(golden, tmp_path):
     finally:
         nat.stop()
         py.stop()
+
+
+def test_lgbserver_large_inputs_body_native(golden, tmp_path):
+    """An lgbserver {"inputs": ...} body of more than 1 MB also takes the
+    native route (kf_parse_inputs on the IO thread), bytes equal to the
+    asyncio server's."""
+    from tests.test_lgb_batching import _lgb_model
+    runs = []
+    for native in (True, False):
+        srv = KFServer(max_batchsize=1 << 16, max_latency_ms=3)
+        srv.native_http = native
+        (tmp_path / ("n" if native else "p")).mkdir()
+        srv.register_model(_lgb_model(golden, tmp_path / ("n" if native else "p")))
+        runs.append(_Running(srv))
+    nat, py = runs
+    _wait_front_end(nat)
+    names = ["sepal_length_(cm)", "sepal_width_(cm)", "petal_length_(cm)", "petal_width_(cm)"]
+    rng = np.random.default_rng(5)
+    cols = {n: rng.uniform(0, 7, 45000).round(4).tolist() for n in names}
+    body = json.dumps({"inputs": [cols]}).encode()
+    assert len(body) > 1 << 20
+    name = nat.server.front_end.app.models.get_models()[0].name
+    path = f"/v1/models/{name}:predict"
+    try:
+        small = json.dumps({"inputs": [{n: [1.0] for n in names}]}).encode()
+        assert nat.fetch(path, "POST", small)[0] == 200                 # the route
+        before = nat.server.front_end.stats()
+        a = nat.fetch(path, "POST", body)
+        b = py.fetch(path, "POST", body)
+        assert a[0] == b[0] == 200 and dict(a[1].items()) == dict(b[1].items())
+        assert _norm(a[2]) == _norm(b[2])
+        st = nat.server.front_end.stats()
+        assert st["native_requests"] - before["native_requests"] == 1
+        assert st["python_requests"] == before["python_requests"]
+    finally:
+        nat.stop()
+        py.stop()
