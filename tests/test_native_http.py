@@ -291,6 +291,20 @@ def test_reload_moves_the_route_to_the_new_batcher(golden, tmp_path):
         n0 = fe.stats()["native_requests"]
         assert nat.fetch("/v1/models/xgboost-iris:predict", "POST", body)[0] == 200
         assert fe.stats()["native_requests"] == n0 + 1
+        # the V2 tensor route follows its batcher through a reload too
+        tb = _v2([[6.8, 2.8, 4.8, 1.4]], [1, 4], "FP32")
+        v2p = "/v2/models/xgboost-iris/infer"
+        first_v2 = nat.fetch(v2p, "POST", tb)
+        assert first_v2[0] == 200 and "v2:xgboost-iris" in fe.routes
+        assert nat.fetch("/v2/repository/models/xgboost-iris/load", "POST", b"")[0] == 200
+        assert "v2:xgboost-iris" not in fe.routes
+        again = nat.fetch(v2p, "POST", tb)                  # through the application
+        assert again[0] == 200 and again[2] == first_v2[2]
+        tnb = fe.app._batchers[("xgboost-iris", "tensor")]
+        assert fe.routes["v2:xgboost-iris"].value == tnb._nb._h.value
+        n1 = fe.stats()["native_requests"]
+        assert nat.fetch(v2p, "POST", tb)[2] == first_v2[2]
+        assert fe.stats()["native_requests"] == n1 + 1
     finally:
         nat.stop()
 
