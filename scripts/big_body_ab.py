@@ -74,12 +74,76 @@ def run_server(native: bool, port: int, tmp: str, rows_list, repeats: int):
     return out
 
 
+def concurrent(native: bool, port: int, tmp: str, rows: int, clients: int, seconds: float):
+    """`clients` keep-alive connections, each sending `rows`-row requests back
+    to back for `seconds`: whole-server rows/s and request latency."""
+    import threading
+    env = dict(os.environ, KF_NATIVE_HTTP="1" if native else "0")
+    cmd = [sys.executable, "-m", "kfserving_amd.xgbserver", "--model_dir", tmp,
+           "--model_name", "model", "--http_port", str(port), "--workers", "1" if native else "8",
+           "--max_batchsize", "65536", "--max_latency_ms", "5", "--http_io_threads", "16"]
+    srv = subprocess.Popen(cmd, cwd=ROOT, env=env, start_new_session=True,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        if not bs.wait_ready(port, 120):
+            raise RuntimeError("server not ready")
+        bs.warm(port, 28)
+        X = np.random.default_rng(3).standard_normal((rows, 28)).astype(np.float32)
+        body = json.dumps({"instances": X.tolist()}).encode()
+        lat, stop = [], time.perf_counter() + seconds
+        lock = threading.Lock()
+
+        def client():
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=120)
+            mine = []
+            while time.perf_counter() < stop:
+                t0 = time.perf_counter()
+                c.request("POST", "/v1/models/model:predict", body=body,
+                          headers={"Content-Type": "application/json"})
+                r = c.getresponse()
+                r.read()
+                if r.status != 200:
+                    raise RuntimeError(f"status {r.status}")
+                mine.append(time.perf_counter() - t0)
+            c.close()
+            with lock:
+                lat.extend(mine)
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=client) for _ in range(clients)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        wall = time.perf_counter() - t0
+        lat_ms = np.asarray(lat) * 1e3
+        return {"server": "native front end" if native else "asyncio (8 workers)",
+                "rows": rows, "clients": clients, "requests": len(lat),
+                "rows_per_s": len(lat) * rows / wall, "p50_ms": float(np.percentile(lat_ms, 50)),
+                "p99_ms": float(np.percentile(lat_ms, 99))}
+    finally:
+        os.killpg(srv.pid, 15)
+        srv.wait(timeout=30)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rows", default="4096,65536")
     p.add_argument("--repeats", type=int, default=10)
     p.add_argument("--port", type=int, default=18300)
+    p.add_argument("--clients", type=int, default=0,
+                   help="> 0: that many concurrent clients of --rows rows each (one size)")
+    p.add_argument("--seconds", type=float, default=8.0)
     a = p.parse_args()
+    if a.clients > 0:
+        tmp = tempfile.mkdtemp()
+        bs.write_c2_model(tmp)
+        for rep in range(2):
+            for native in (True, False):
+                r = concurrent(native, a.port + 2 * rep + int(native), tmp, int(a.rows),
+                               a.clients, a.seconds)
+                r["round"] = rep
+                print(json.dumps(r), flush=True)
+        return
     rows_list = [int(r) for r in a.rows.split(",")]
     tmp = tempfile.mkdtemp()
     bs.write_c2_model(tmp)
