@@ -74,14 +74,17 @@ def run_server(native: bool, port: int, tmp: str, rows_list, repeats: int):
     return out
 
 
-def concurrent(native: bool, port: int, tmp: str, rows: int, clients: int, seconds: float):
+def concurrent(native: bool, port: int, tmp: str, rows: int, clients: int, seconds: float,
+               native_workers: int = 1):
     """`clients` keep-alive connections, each sending `rows`-row requests back
     to back for `seconds`: whole-server rows/s and request latency."""
     import threading
     env = dict(os.environ, KF_NATIVE_HTTP="1" if native else "0")
     cmd = [sys.executable, "-m", "kfserving_amd.xgbserver", "--model_dir", tmp,
-           "--model_name", "model", "--http_port", str(port), "--workers", "1" if native else "8",
-           "--max_batchsize", "65536", "--max_latency_ms", "5", "--http_io_threads", "16"]
+           "--model_name", "model", "--http_port", str(port),
+           "--workers", str(native_workers) if native else "8",
+           "--max_batchsize", "65536", "--max_latency_ms", "5",
+           "--http_io_threads", str(max(2, 16 // native_workers))]
     srv = subprocess.Popen(cmd, cwd=ROOT, env=env, start_new_session=True,
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     try:
@@ -116,7 +119,8 @@ def concurrent(native: bool, port: int, tmp: str, rows: int, clients: int, secon
             t.join()
         wall = time.perf_counter() - t0
         lat_ms = np.asarray(lat) * 1e3
-        return {"server": "native front end" if native else "asyncio (8 workers)",
+        return {"server": f"native front end ({native_workers} workers)" if native
+                else "asyncio (8 workers)",
                 "rows": rows, "clients": clients, "requests": len(lat),
                 "rows_per_s": len(lat) * rows / wall, "p50_ms": float(np.percentile(lat_ms, 50)),
                 "p99_ms": float(np.percentile(lat_ms, 99))}
@@ -133,6 +137,7 @@ def main():
     p.add_argument("--clients", type=int, default=0,
                    help="> 0: that many concurrent clients of --rows rows each (one size)")
     p.add_argument("--seconds", type=float, default=8.0)
+    p.add_argument("--native-workers", type=int, default=1)
     a = p.parse_args()
     if a.clients > 0:
         tmp = tempfile.mkdtemp()
@@ -140,7 +145,7 @@ def main():
         for rep in range(2):
             for native in (True, False):
                 r = concurrent(native, a.port + 2 * rep + int(native), tmp, int(a.rows),
-                               a.clients, a.seconds)
+                               a.clients, a.seconds, a.native_workers)
                 r["round"] = rep
                 print(json.dumps(r), flush=True)
         return
