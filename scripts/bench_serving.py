@@ -53,11 +53,17 @@ def body_of(X, protocol="v1"):
         return json.dumps({"inputs": [{"name": "input-0", "shape": list(X.shape),
                                        "datatype": "FP32",
                                        "data": X.reshape(-1).tolist()}]}).encode()
+    if protocol == "v2bin":   # u32 head length, JSON head, raw little-endian FP32 rows
+        raw = np.ascontiguousarray(X, dtype="<f4").tobytes()
+        head = json.dumps({"inputs": [{"name": "input-0", "shape": list(X.shape),
+                                       "datatype": "FP32",
+                                       "parameters": {"binary_data_size": len(raw)}}]}).encode()
+        return struct.pack("<I", len(head)) + head + raw
     return json.dumps({"instances": X.tolist()}).encode()
 
 
 def predict_path(protocol="v1", model="model"):
-    return f"/v2/models/{model}/infer" if protocol == "v2" else f"/v1/models/{model}:predict"
+    return f"/v2/models/{model}/infer" if protocol != "v1" else f"/v1/models/{model}:predict"
 
 
 def write_bodies(path, n_feat, variants, seed, protocol="v1"):
@@ -99,10 +105,15 @@ def wait_ready(port, timeout=180):
 
 def warm(port, n_feat, n=20, protocol="v1"):
     body = body_of(np.zeros((64, n_feat), dtype=np.float32), protocol)
+    hdrs = {"Content-Type": "application/json"}
+    if protocol == "v2bin":
+        head = struct.unpack("<I", body[:4])[0]
+        body = body[4:]
+        hdrs = {"Content-Type": "application/octet-stream",
+                "Inference-Header-Content-Length": str(head)}
     for _ in range(n):
         c = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
-        c.request("POST", predict_path(protocol), body=body,
-                  headers={"Content-Type": "application/json"})
+        c.request("POST", predict_path(protocol), body=body, headers=hdrs)
         r = c.getresponse()
         r.read()
         c.close()
@@ -145,14 +156,16 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
                                   "--qps", str(q), "--duration", str(duration),
                                   "--warmup", str(warmup), "--bodies", bodies,
                                   "--threads", str(loadgen_threads),
-                                  "--path", predict_path(protocol)],
+                                  "--path", predict_path(protocol),
+                                  "--v2-binary", "1" if protocol == "v2bin" else "0"],
                                  capture_output=True, text=True,
                                  timeout=duration + warmup + 60)   # loadgen drains by +30 s
             if out.returncode != 0:
                 raise RuntimeError(f"loadgen failed: {out.stderr[-2000:]}")
             res = json.loads(out.stdout)
-            res.update({"config": ("C5 dynamic batching: V2 /infer FP32 JSON tensors" if
-                                   protocol == "v2" else "C5 dynamic batching: v1 :predict") +
+            res.update({"config": {"v2": "C5 dynamic batching: V2 /infer FP32 JSON tensors",
+                                   "v2bin": "C5 dynamic batching: V2 /infer FP32 binary tensors"}
+                        .get(protocol, "C5 dynamic batching: v1 :predict") +
                                   " over HTTP, KFServer in-process batcher", "model": model,
                         "protocol": protocol,
                         "workers": workers, "max_batch_size": max_batch,
@@ -193,8 +206,8 @@ def main():
     p.add_argument("--io-threads", type=int, default=2,
                    help="native HTTP front end IO threads per worker (KF_NATIVE_HTTP=0: "
                         "the asyncio server)")
-    p.add_argument("--protocol", default="v1", choices=["v1", "v2"],
-                   help="v1 :predict instances, or V2 /infer FP32 JSON tensors")
+    p.add_argument("--protocol", default="v1", choices=["v1", "v2", "v2bin"],
+                   help="v1 :predict instances, V2 /infer FP32 JSON tensors, or V2 binary tensors")
     args = p.parse_args()
     serve_and_measure([float(x) for x in args.qps.split(",")], args.workers, args.io_threads,
                       args.duration, args.warmup, args.conns, args.port, args.model,

@@ -247,6 +247,9 @@ int main(int argc, char** argv) {
   double dur = atof(arg(argc, argv, "--duration", "10"));
   double warm = atof(arg(argc, argv, "--warmup", "2"));
   const char* bodies = arg(argc, argv, "--bodies", "bodies.bin");
+  // --v2-binary: each body starts with a u32, the length of its JSON head (the
+  // V2 binary tensor extension's Inference-Header-Content-Length)
+  const int v2bin = atoi(arg(argc, argv, "--v2-binary", "0"));
 
   struct rlimit rl;
   getrlimit(RLIMIT_NOFILE, &rl);
@@ -268,12 +271,26 @@ int main(int argc, char** argv) {
       if (fread(body, 1, bl, f) != bl) { fprintf(stderr, "short bodies file\n"); return 2; }
       Req* q = &reqs[(r - 1) * nv + v];
       char hdr[512];
-      int hl = snprintf(hdr, sizeof hdr,
-                        "POST %s HTTP/1.1\r\nHost: %s:%d\r\nContent-Type: application/json\r\n"
-                        "Content-Length: %u\r\n\r\n", path, host, port, bl);
+      const char* b = body;
+      int hl;
+      if (v2bin) {
+        uint32_t head;
+        if (bl < 4) { fprintf(stderr, "bad binary body\n"); return 2; }
+        memcpy(&head, body, 4);
+        b = body + 4;
+        bl -= 4;
+        hl = snprintf(hdr, sizeof hdr,
+                      "POST %s HTTP/1.1\r\nHost: %s:%d\r\nContent-Type: application/octet-stream\r\n"
+                      "Inference-Header-Content-Length: %u\r\nContent-Length: %u\r\n\r\n", path,
+                      host, port, head, bl);
+      } else {
+        hl = snprintf(hdr, sizeof hdr,
+                      "POST %s HTTP/1.1\r\nHost: %s:%d\r\nContent-Type: application/json\r\n"
+                      "Content-Length: %u\r\n\r\n", path, host, port, bl);
+      }
       q->req = malloc((size_t)hl + bl);
       memcpy(q->req, hdr, (size_t)hl);
-      memcpy(q->req + hl, body, bl);
+      memcpy(q->req + hl, b, bl);
       q->len = hl + (int)bl;
       q->rows = r;
       free(body);
