@@ -148,8 +148,18 @@ def parse_args(argv=None):
     p.add_argument("--host-rows", type=int, default=8_000_000,
                    help="rows of the host-to-host (PCIe-inclusive) C2 leg (0 = skip)")
     p.add_argument("--c5-http-qps", default="20000,100000,200000",
-                   help="C5 over HTTP: offered req/s of the points (empty: skip); rank 0, "
-                        "after the GPU legs, a server of one worker per GPU")
+                   help="C5 over HTTP: offered req/s PER GPU of the points (x N for the node; "
+                        "empty: skip); rank 0, after the GPU legs, a server of one worker per GPU")
+    p.add_argument("--c5-conns-per-gpu", type=int, default=4096,
+                   help="C5 over HTTP: keep-alive client connections per GPU")
+    p.add_argument("--c5-loadgen-threads-per-gpu", type=int, default=4)
+    p.add_argument("--c5-io-threads", type=int, default=16,
+                   help="native HTTP IO threads per worker (the one-GPU value at every N)")
+    p.add_argument("--c5-capacity-points", type=int, default=3,
+                   help="C5 over HTTP: extra points searching the highest offered rate with "
+                        "p99 <= 2 x maxLatency and no loss (0 = no search)")
+    p.add_argument("--c5-http-cpu", action="store_true",
+                   help="--device cpu: run the C5 HTTP leg against the CPU echo model (tests)")
     p.add_argument("--c5-http-seconds", type=float, default=4.0)
     p.add_argument("--c5-http-v2-qps", default="100000",
                    help="the same with V2 FP32 JSON tensor bodies on /v2/models/<name>/infer "
@@ -651,47 +661,72 @@ def native_batched_latency(dev, n_feat, qps, seconds, max_batch=65536, max_laten
             "_lat_ms": lat_ms}
 
 
-def c5_http_leg(args, world, protocol="v1"):
+def c5_http_leg(args, world, protocol="v1", device="cuda"):
     """BASELINE config C5 as named, over HTTP: xgbserver with the C2 forest
     (`python -m kfserving_amd.xgbserver`, --max_batchsize 65536
     --max_latency_ms 5) behind the native HTTP front end and native batcher,
-    one worker process per GPU of the job (worker i drives GPU i), 4,096
-    keep-alive connections from the C load generator (scripts/loadgen.c:
-    open-loop Poisson arrivals of U{1..64}-row v1 :predict bodies, latency
-    from the scheduled arrival; 4 threads, each its own epoll loop), 16 IO
-    threads over the workers.  Run on rank 0 after every rank's GPU legs; the
-    offered rates are totals for the node, not per GPU."""
-    import torch
+    one worker process per GPU of the job (worker i drives GPU i), keep-alive
+    connections from the C load generator (scripts/loadgen.c: open-loop
+    Poisson arrivals of U{1..64}-row v1 :predict bodies, latency from the
+    scheduled arrival; each thread its own epoll loop).  Run on rank 0 after
+    every rank's GPU legs.
+
+    Sized with N: the points are per-GPU rates x N (the
+    node offered 1.6M req/s at N = 8 for the 200k per-GPU point), 4,096
+    connections and 4 load-generator threads per GPU, and every worker keeps
+    the one-GPU worker's 16 IO threads.  After the fixed points the same
+    server searches the node's capacity: the highest offered rate with p99 <=
+    2 x maxLatency and no request lost (scripts/bench_serving.capacity_search;
+    reference pkg/batcher/handler.go:156-185, kfserver.py:99 start(workers)).
+    `--device cpu` (tests) serves bench_serving's CPU echo model instead."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import bench_serving as bs
     env = dict(os.environ)
-    if world == 1:
+    if world == 1 and device != "cpu":
+        import torch
         env["TREEINFER_DEVICES"] = str(torch.cuda.current_device())
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
               "MASTER_PORT", "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
     spec = args.c5_http_v2_qps if protocol == "v2" else args.c5_http_qps
-    qps = [float(q) for q in spec.split(",") if q.strip()]
-    io = max(2, 16 // world)
+    per_gpu = [float(q) for q in spec.split(",") if q.strip()]
+    qps = [q * world for q in per_gpu]
+    io = args.c5_io_threads
+    conns = args.c5_conns_per_gpu * world
+    lg_threads = args.c5_loadgen_threads_per_gpu * world
+    cap = {}
     try:
         pts = bs.serve_and_measure(qps, workers=world, io_threads=io,
-                                   duration=args.c5_http_seconds, warmup=1.5, conns=4096,
+                                   duration=args.c5_http_seconds, warmup=1.5, conns=conns,
                                    port=18090 + (os.getpid() % 500) + (600 if protocol == "v2" else 0),
-                                   env=env, ready_timeout=90, loadgen_threads=4, echo=False,
-                                   protocol=protocol)
+                                   env=env, ready_timeout=90, loadgen_threads=lg_threads,
+                                   echo=False, protocol=protocol,
+                                   model="dummy" if device == "cpu" else "c2",
+                                   capacity_points=(args.c5_capacity_points
+                                                    if protocol == "v1" else 0),
+                                   capacity_out=cap)
     except Exception as e:   # reported, not fatal: the headline stands without it
         return {"error": str(e)[-500:]}
     keep = ("offered_qps", "req_per_s", "rows_per_s", "p50_ms", "p90_ms", "p99_ms", "max_ms",
             "requests", "lost", "non200", "conn_errors")
-    return {"devices": world, "workers": world, "io_threads_per_worker": io,
-            "conns": 4096, "loadgen_threads": 4, "rows_per_request": "U{1..64}",
-            "max_batch_size": 65536,
-            "max_latency_ms": 5, "model": "C2 (500 x depth 8, 28 features), xgbserver",
-            "path": "HTTP/1.1 keep-alive -> native front end (kfhttp.h) -> native batcher "
-                    "(kfbatch.h) -> ti_predict (host buffers)",
-            "protocol": ("V2 /infer, one FP32 tensor of JSON data" if protocol == "v2"
-                         else "v1 :predict instances"),
-            "points": [{k: p.get(k) for k in keep} for p in pts]}
+    res = {"devices": world, "workers": world, "io_threads_per_worker": io,
+           "conns": conns, "conns_per_gpu": args.c5_conns_per_gpu,
+           "loadgen_threads": lg_threads, "rows_per_request": "U{1..64}",
+           "offered_qps_per_gpu": per_gpu, "offered_qps_node": qps,
+           "max_batch_size": 65536,
+           "max_latency_ms": 5, "model": ("C2 (500 x depth 8, 28 features), xgbserver"
+                                          if device != "cpu" else "CPU echo model (tests)"),
+           "path": "HTTP/1.1 keep-alive -> native front end (kfhttp.h) -> native batcher "
+                   "(kfbatch.h) -> ti_predict (host buffers)",
+           "protocol": ("V2 /infer, one FP32 tensor of JSON data" if protocol == "v2"
+                        else "v1 :predict instances"),
+           "points": [{k: p.get(k) for k in keep} for p in pts]}
+    if cap:
+        c = cap.get("capacity_req_per_s")
+        res["capacity_req_per_s"] = c
+        res["capacity_req_per_s_per_gpu"] = None if c is None else c / world
+        res["capacity"] = cap
+    return res
 
 
 def tree_shard_leg(forest, dev, rows, args, world, rank, local_rank, device, dev_sync,
@@ -731,11 +766,14 @@ def tree_shard_leg(forest, dev, rows, args, world, rank, local_rank, device, dev
                "collective": "dist.reduce(SUM) of [rows, K] float32 partial margins to rank 0"
                              if world > 1 else "none (one rank)",
                "path": "kfserving_amd.tree_shard.TreeShardedForest"}
-        if device != "cpu":
+        # the check runs on the GPU, and on CPU with an engine that computes
+        # (tests/bench_stub.py:make_canon), not with the sleeping stand-in
+        if device != "cpu" or getattr(dev, "computes", False):
             ref = torch.empty(rows, dtype=torch.float32, device=device)
             dev.predict_device(X.data_ptr(), TI_F32, rows, N_FEAT, N_FEAT, OUT_PREDICT,
                                ref.data_ptr(), rows, slot=0,
-                               stream=torch.cuda.current_stream().cuda_stream)
+                               stream=(torch.cuda.current_stream().cuda_stream
+                                       if device != "cpu" else 0))
             dev_sync()
             got = out[0].reshape(-1).double()
             want = ref.double()
@@ -1222,10 +1260,11 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
     if rank != 0:
         return None
     c5_http = c5_http_v2 = None
-    if args.c5_http_qps and device != "cpu":
-        c5_http = c5_http_leg(args, world)
-    if args.c5_http_v2_qps and device != "cpu":
-        c5_http_v2 = c5_http_leg(args, world, "v2")
+    http_ok = device != "cpu" or args.c5_http_cpu
+    if args.c5_http_qps and http_ok:
+        c5_http = c5_http_leg(args, world, device=device)
+    if args.c5_http_v2_qps and http_ok:
+        c5_http_v2 = c5_http_leg(args, world, "v2", device=device)
     cpu = None
     if not args.no_cpu_baseline:
         cpu = cpu_baseline(trees, ti, X_host, args.cpu_seconds)

@@ -14,8 +14,9 @@ library's own output transform (``ti_transform_device``) runs there.
 
 Numerics: each rank sums its trees in order and the reduce adds the partial
 sums, so margins differ from the one-device order by rounding only
-(north_star: within 1e-5 relative); leaf ids are gathered, not summed, and stay
-exact.  TreeSHAP contributions are additive over trees too (each shard's bias
+(north_star: within 1e-5 relative); leaf ids are gathered to the root (a
+``gather``, so each rank sends its block once and only the root receives), not
+summed, and stay exact.  TreeSHAP contributions are additive over trees too (each shard's bias
 holds its trees' expected values; the base margin lives on the root's shard)
 and are reduced the same way.
 
@@ -138,13 +139,18 @@ class TreeShardedForest:
         local[:, :t1 - t0] = mine
         if self.world == 1:
             return mine
+        # a gather to the root, not an all_gather: only the root uses the ids,
+        # so each rank sends its [rows, tmax] block once and receives nothing
+        is_root = self.rank == self.root
         if local.is_cuda and self._gloo():   # gloo gathers host tensors only
-            bufs = [torch.empty_like(local, device="cpu") for _ in range(self.world)]
-            dist.all_gather(bufs, local.cpu(), group=self.group)
-            bufs = [b.to(X.device) for b in bufs]
+            bufs = ([torch.empty_like(local, device="cpu") for _ in range(self.world)]
+                    if is_root else None)
+            dist.gather(local.cpu(), gather_list=bufs, dst=self.root, group=self.group)
+            if is_root:
+                bufs = [b.to(X.device) for b in bufs]
         else:
-            bufs = [torch.empty_like(local) for _ in range(self.world)]
-            dist.all_gather(bufs, local, group=self.group)
-        if self.rank != self.root:
+            bufs = [torch.empty_like(local) for _ in range(self.world)] if is_root else None
+            dist.gather(local, gather_list=bufs, dst=self.root, group=self.group)
+        if not is_root:
             return None
         return torch.cat([bufs[r][:, :b - a] for r, (a, b) in enumerate(self.ranges)], dim=1)

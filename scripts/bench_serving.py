@@ -121,11 +121,62 @@ def warm(port, n_feat, n=20, protocol="v1"):
             raise RuntimeError(f"warm-up predict returned {r.status}")
 
 
+def point_passes(res, p99_bound_ms):
+    """A capacity-search point holds when its p99 is within the bound and no
+    request was lost, failed or answered non-200."""
+    return (res.get("p99_ms") is not None and res["p99_ms"] <= p99_bound_ms
+            and not res.get("lost") and not res.get("non200") and not res.get("conn_errors"))
+
+
+def capacity_search(measure, done, p99_bound_ms, points, grow=1.5, resolution=1.1):
+    """The highest offered rate whose point passes (`point_passes`), searched
+    after the fixed points `done` [(qps, result)]: from the best passing rate,
+    grow by `grow` until a point fails, then bisect (geometric midpoint)
+    between the best pass and the lowest fail until they are within
+    `resolution` or `points` more runs are spent.  `measure(qps)` runs one
+    point.  Returns {capacity_req_per_s, first_fail_req_per_s, searched}."""
+    ok = [q for q, r in done if point_passes(r, p99_bound_ms)]
+    bad = [q for q, r in done if not point_passes(r, p99_bound_ms)]
+    lo = max(ok) if ok else None
+    hi = min([q for q in bad if lo is None or q > lo], default=None)
+    searched = []
+    for _ in range(max(0, points)):
+        if lo is None:                       # even the lowest fixed point failed
+            if hi is None:
+                break
+            q = hi / 2.0
+        elif hi is None:
+            q = lo * grow
+        else:
+            if hi / lo <= resolution:
+                break
+            q = (lo * hi) ** 0.5
+        q = float(round(q, -2)) if q >= 1000 else float(round(q))
+        try:
+            r = measure(q)
+        except Exception as e:              # a point the load generator could not finish
+            r = {"error": str(e)[-300:]}
+        passed = point_passes(r, p99_bound_ms)
+        searched.append({"offered_qps": q, "p99_ms": r.get("p99_ms"), "lost": r.get("lost"),
+                         "non200": r.get("non200"), "req_per_s": r.get("req_per_s"),
+                         "passed": passed, **({"error": r["error"]} if "error" in r else {})})
+        if passed:
+            lo = q if lo is None else max(lo, q)
+        else:
+            hi = q if hi is None else min(hi, q)
+    return {"capacity_req_per_s": lo, "first_fail_req_per_s": hi,
+            "criterion": f"p99 <= {p99_bound_ms:g} ms (2 x maxLatency), 0 lost, 0 non-200",
+            "searched": searched}
+
+
 def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.0, conns=4096,
                       port=18080, model="c2", max_batch=65536, max_latency_ms=5, env=None,
-                      ready_timeout=180, loadgen_threads=1, echo=True, protocol="v1"):
+                      ready_timeout=180, loadgen_threads=1, echo=True, protocol="v1",
+                      capacity_points=0, capacity_out=None):
     """Start the server, drive it with the C load generator at each offered
-    rate in turn, stop it; one result dict per rate."""
+    rate in turn, stop it; one result dict per rate.  With capacity_points > 0
+    the same server then runs `capacity_search` (p99 <= 2 x maxLatency, no
+    loss) for up to that many more points and fills `capacity_out`."""
     soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
     resource.setrlimit(resource.RLIMIT_NOFILE, (hard, hard))
     n_feat = 28
@@ -151,7 +202,8 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
             raise RuntimeError("server did not become ready: " +
                                open(os.path.join(tmp, "server.log")).read()[-2000:])
         warm(port, n_feat, protocol=protocol)
-        for q in qps_list:
+
+        def measure(q):
             out = subprocess.run([LOADGEN, "--port", str(port), "--conns", str(conns),
                                   "--qps", str(q), "--duration", str(duration),
                                   "--warmup", str(warmup), "--bodies", bodies,
@@ -174,9 +226,19 @@ def serve_and_measure(qps_list, workers=4, io_threads=2, duration=8.0, warmup=2.
                         "native_batcher": env.get("KF_NATIVE_BATCHER", "1") != "0",
                         "io_threads": io_threads, "loadgen_threads": loadgen_threads,
                         "gpus_visible": env.get("TREEINFER_DEVICES", "all")})
-            results.append(res)
             if echo:   # bench.py's leg prints nothing of its own (one JSON line)
                 print(json.dumps(res), flush=True)
+            return res
+
+        for q in qps_list:
+            results.append(measure(q))
+        if capacity_points > 0:
+            cap = capacity_search(measure, list(zip(qps_list, results)), 2.0 * max_latency_ms,
+                                  capacity_points)
+            if capacity_out is not None:
+                capacity_out.update(cap)
+            if echo:
+                print(json.dumps({"capacity": cap}), flush=True)
     finally:
         try:
             os.killpg(server.pid, signal.SIGTERM)
@@ -208,11 +270,14 @@ def main():
                         "the asyncio server)")
     p.add_argument("--protocol", default="v1", choices=["v1", "v2", "v2bin"],
                    help="v1 :predict instances, V2 /infer FP32 JSON tensors, or V2 binary tensors")
+    p.add_argument("--capacity-points", type=int, default=0,
+                   help="after the fixed points, search this many more for the highest rate "
+                        "with p99 <= 2 x maxLatency and no loss")
     args = p.parse_args()
     serve_and_measure([float(x) for x in args.qps.split(",")], args.workers, args.io_threads,
                       args.duration, args.warmup, args.conns, args.port, args.model,
                       args.max_batch, args.max_latency_ms, loadgen_threads=args.loadgen_threads,
-                      protocol=args.protocol)
+                      protocol=args.protocol, capacity_points=args.capacity_points)
 
 
 if __name__ == "__main__":

@@ -35,3 +35,27 @@ class StubEngine:
 
 def make(forest, local_rank):
     return StubEngine(forest, local_rank)
+
+
+class CanonStubEngine(StubEngine):
+    """The stand-in that also computes: predict_device on CPU tensors through
+    the canonical numpy evaluator (tests/canon_eval.py), so bench.py's
+    tree-sharded leg can check its reduced margins at --device cpu
+    (`--engine tests.bench_stub:make_canon`)."""
+    computes = True
+
+    def predict_device(self, x_ptr, x_dtype, n_rows, n_cols, row_stride, kind, out_ptr,
+                       out_len, slot=0, stream=0):
+        from tests.test_tree_shard import CanonEngine
+        super().predict_device(x_ptr, x_dtype, n_rows, n_cols, row_stride, kind, out_ptr,
+                               out_len)
+        CanonEngine(self.forest, None).predict_device(x_ptr, x_dtype, n_rows, n_cols,
+                                                      row_stride, kind, out_ptr, out_len)
+
+    def transform_device(self, margin_ptr, n_rows, out_ptr, out_len, slot=0, stream=0):
+        from tests.test_tree_shard import CanonEngine
+        CanonEngine(self.forest, None).transform_device(margin_ptr, n_rows, out_ptr, out_len)
+
+
+def make_canon(forest, local_rank):
+    return CanonStubEngine(forest, local_rank)

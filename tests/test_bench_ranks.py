@@ -150,6 +150,68 @@ def test_bench_cli_gpus_n_starts_n_ranks():
     assert 0 < ts["trees_rank0"] < 500
 
 
+def test_bench_cli_world2_c5_scales_and_tree_shard_checks():
+    """VERDICT r5 items 1 and 8 through the CLI at world 2 (gloo, CPU): the
+    C5-over-HTTP leg offers per-GPU rates x N with connections and load
+    generator threads per GPU and the one-GPU IO thread count, and searches
+    the capacity; the tree-sharded leg's reduced predictions are checked
+    against the replicated forest (an engine that computes on CPU)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_serving as bs
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "4"
+    http = os.path.exists(bs.LOADGEN)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--engine", "tests.bench_stub:make_canon", "--steps", "2", "--warmup", "1",
+           "--rows", "1024", "--configs", "", "--no-cpu-baseline", "--latency-qps", "0",
+           "--nan-variant", "0", "--host-rows", "0", "--c5-http-v2-qps", "",
+           "--c5-http-qps", "100,200" if http else "", "--c5-http-cpu",
+           "--c5-conns-per-gpu", "16", "--c5-loadgen-threads-per-gpu", "1",
+           "--c5-io-threads", "2", "--c5-capacity-points", "1", "--c5-http-seconds", "0.5"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    ts = line["tree_shard"]
+    assert ts["ranks"] == 2 and ts["within_1e-5"] is True, ts
+    assert ts["max_rel_diff_vs_replicated"] <= 1e-5
+    if not http:
+        pytest.skip("loadgen not built: the C5 HTTP half is not exercised")
+    c5 = line["c5_http"]
+    assert "error" not in c5, c5
+    assert c5["devices"] == 2 and c5["workers"] == 2
+    assert c5["offered_qps_per_gpu"] == [100.0, 200.0]
+    assert c5["offered_qps_node"] == [200.0, 400.0]                # doubled at world 2
+    assert [p["offered_qps"] for p in c5["points"]] == [200.0, 400.0]
+    assert c5["conns"] == 32 and c5["loadgen_threads"] == 2
+    assert c5["io_threads_per_worker"] == 2                       # not divided by N
+    cap = c5["capacity"]
+    assert len(cap["searched"]) <= 1 and "criterion" in cap
+    assert c5["capacity_req_per_s"] == cap["capacity_req_per_s"]
+
+
+def test_capacity_search_grows_then_bisects():
+    """bench_serving.capacity_search on a synthetic server whose p99 crosses
+    10 ms at 250k req/s: grows from the best fixed point, then bisects."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_serving as bs
+
+    def fake(q):
+        return {"p99_ms": 5.3 if q <= 250_000 else 40.0, "lost": 0, "non200": 0,
+                "conn_errors": 0, "req_per_s": q}
+    done = [(q, fake(q)) for q in (20_000, 100_000, 200_000)]
+    cap = bs.capacity_search(fake, done, 10.0, points=6)
+    assert 200_000 <= cap["capacity_req_per_s"] <= 250_000
+    assert cap["first_fail_req_per_s"] > 250_000
+    assert cap["searched"][0]["offered_qps"] == 300_000 and not cap["searched"][0]["passed"]
+    assert cap["first_fail_req_per_s"] / cap["capacity_req_per_s"] <= 1.25
+    # a lost request fails a point whatever its p99
+    assert not bs.point_passes({"p99_ms": 1.0, "lost": 3, "non200": 0}, 10.0)
+    # nothing passes: halve from the lowest failure
+    cap = bs.capacity_search(lambda q: {"p99_ms": 99.0}, [(1000.0, {"p99_ms": 99.0})], 10.0, 2)
+    assert cap["capacity_req_per_s"] is None and [s["offered_qps"] for s in cap["searched"]] == [500.0, 250.0]
+
+
 def test_headline_defaults_two_streams():
     """The headline keeps two batches in flight by default (DESIGN.md section
     4); without a GPU there is one stream and the two timings coincide."""

@@ -63,6 +63,10 @@ def _forest(K):
 def _worker(rank, world, port, K, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def no_all_gather(*a, **k):   # leaf ids go to the root alone
+        raise AssertionError("tree_shard must gather to the root, not all_gather")
+    dist.all_gather = no_all_gather
     from kfserving_amd.tree_shard import TreeShardedForest
     f = _forest(K)
     ts = TreeShardedForest(f, engine_factory=CanonEngine)
