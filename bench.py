@@ -89,8 +89,7 @@ def launched_kernel(info: dict) -> str:
     if layout == 3:
         return WALK_KERNELS.get(info.get("walk"), "bheap_predict_kernel")
     if layout == 9:
-        return {1: "t8explicit_predict_kernel", 2: "t16explicit_predict_kernel",
-                3: "t16lane_predict_kernel"}.get(
+        return {1: "t8explicit_predict_kernel", 2: "t16explicit_predict_kernel"}.get(
             info.get("bottom"), "texplicit_predict_kernel")
     return LAYOUT_KERNELS.get(layout, f"layout{layout}")
 

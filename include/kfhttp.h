@@ -110,8 +110,11 @@ int kh_add_v2_tensor_predict(void* srv, const char* model, void* batcher, int32_
 
 /* Stop answering the model natively (its requests go to the application):
  * the batcher's forming batch is flushed, the requests already submitted are
- * answered, and the batcher's done callback is detached before this returns,
- * so the caller may then destroy the batcher. */
+ * answered, and the batcher's done callback is detached before this returns
+ * 0, so the caller may then destroy the batcher.  -2: requests were still on
+ * the batcher after 20 s; the callback stays attached (late completions still
+ * reach their connections), and destroying the batcher (kb_destroy answers
+ * what it holds first) remains safe.  -1: no such route. */
 int kh_remove_route(void* srv, const char* model);
 
 int kh_start(void* srv);

@@ -188,6 +188,15 @@ typedef struct ti_forest_info {
                                      device (0: never); default 1280 or
                                      $TI_SHAP_TABLE_MB; read when a replica's table
                                      is first needed                                */
+#define TI_OPT_HOST_REGISTER   3  /* 1: ti_predict page-locks the caller's X and
+                                     output for a multi-chunk batch and copies
+                                     straight from / to them; 0
+                                     (default): pinned staging chunks.  A buffer
+                                     that cannot be registered, or whose pages
+                                     another registration already holds, takes
+                                     the staging chunks.  The caller must not
+                                     predict concurrently into buffers sharing a
+                                     page with this call's.                         */
 
 /* Upload the forest to each listed device (HIP device ordinals).  HIP is
  * initialised here, not at library load, so a process may fork before it.

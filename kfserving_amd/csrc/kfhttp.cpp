@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <atomic>
 #include <charconv>
+#include <chrono>
 #include <cctype>
 #include <cmath>
 #include <cstdint>
@@ -49,6 +50,14 @@
 namespace {
 
 constexpr size_t kMaxLine = 1u << 20;       // asyncio StreamReader limit (start_server)
+// read backpressure: while a connection's request is being
+// answered, at most this many unparsed bytes are buffered behind it (the
+// asyncio server stops reading past 2 x its 2^20 StreamReader limit); the read
+// resumes once the answer is out
+constexpr size_t kMaxPipelined = size_t(2) << 20;
+// bytes one wake-up reads from a connection before the IO thread serves the
+// others (edge-triggered: the connection is revisited after this epoll round)
+constexpr size_t kReadBudget = size_t(4) << 20;
 constexpr uint64_t kListen = ~0ULL, kWake = ~0ULL - 1;
 constexpr int kThreadShift = 48;            // tag / id: thread index above the connection id
 
@@ -68,6 +77,18 @@ struct Route {
   bool v2 = false;   // V2 tensor requests (kh_add_v2_tensor_predict)
 };
 
+// where an incomplete chunked body stopped (offsets relative to the request's
+// first byte, which stays at Conn::in_off until the request completes), so the
+// next read resumes at the chunk it was in instead of re-parsing them all
+struct ChunkState {
+  bool active = false;
+  size_t next = 0;                                  // the next chunk-size line
+  int64_t total = 0;
+  std::vector<std::pair<size_t, size_t>> spans;     // (offset, size) of the chunks so far
+  std::string method, target, version, headers;
+  std::unordered_map<std::string, std::string> h;
+};
+
 struct Conn {
   uint64_t id = 0;
   int fd = -1;
@@ -79,6 +100,9 @@ struct Conn {
   bool peer_gone = false;    // the peer closed while busy: free on the answer
   bool close_after = false;  // close once `out` is written
   bool want_out = false;     // EPOLLOUT armed
+  bool peer_eof = false;     // the peer shut its side: answer what is complete, then close
+  bool read_paused = false;  // busy with kMaxPipelined bytes behind: resumed by on_done
+  ChunkState chunk;
   // the fast-path request in flight
   Route route;
   std::vector<unsigned char> res;
@@ -110,6 +134,7 @@ struct IoThread {
   std::vector<int> new_fds;      // connections another thread accepted for this one
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;   // this thread only
   uint64_t next_id = 1;
+  std::vector<uint64_t> again;   // connections that used their read budget: read on
 };
 
 struct Pending {
@@ -421,10 +446,21 @@ struct Req {
   size_t need = 0;   // kIncomplete with a Content-Length: the request's whole size
 };
 
-Parse parse_request(const std::string& in, size_t start, int64_t max_body, Req* r) {
+Parse parse_request(const std::string& in, size_t start, int64_t max_body, Req* r,
+                    ChunkState* cs) {
   size_t pos = start;
   std::string line;
-  int k = take_line(in, pos, line);
+  int k;
+  if (cs && cs->active) {   // a chunked body part-way: the head and the chunks so far
+    r->method = cs->method;
+    r->target = cs->target;
+    r->version = cs->version;
+    r->headers = cs->headers;
+    r->h = cs->h;
+    pos = start + cs->next;
+    goto chunks;
+  }
+  k = take_line(in, pos, line);
   if (k == 0) return Parse::kIncomplete;
   if (k < 0) return Parse::kBad;
   {
@@ -454,39 +490,74 @@ Parse parse_request(const std::string& in, size_t start, int64_t max_body, Req* 
     r->headers += val;
     r->headers += '\n';
   }
-  auto te = r->h.find("transfer-encoding");
-  r->body.clear();
-  if (te != r->h.end() && lower(te->second) == "chunked") {
-    // the chunks' spans first; the body is copied only once it is all here
-    // (a body arriving over many reads is re-parsed after each of them)
-    int64_t total = 0;
-    std::vector<std::pair<size_t, size_t>> spans;
+  {
+    auto te = r->h.find("transfer-encoding");
+    if (te == r->h.end() || lower(te->second) != "chunked") goto plain;
+  }
+chunks : {
+    // the chunks' spans first; the body is copied only once it is all here.
+    // An incomplete body saves where it stopped (ChunkState): the next read
+    // resumes at the chunk it was in, so a body of many small chunks costs
+    // O(chunks) over all its reads, not per read
+    r->body.clear();
+    ChunkState local;
+    ChunkState& st = cs ? *cs : local;
+    if (!st.active) {
+      st.total = 0;
+      st.spans.clear();
+    }
+    auto incomplete = [&](size_t chunk_start) {
+      if (cs) {
+        if (!st.active) {
+          st.method = r->method;
+          st.target = r->target;
+          st.version = r->version;
+          st.headers = r->headers;
+          st.h = r->h;
+        }
+        st.active = true;
+        st.next = chunk_start - start;
+      }
+      return Parse::kIncomplete;
+    };
+    auto fail = [&](Parse p) {
+      st.active = false;
+      return p;
+    };
     for (;;) {
+      const size_t chunk_start = pos;
       k = take_line(in, pos, line);
-      if (k == 0) return Parse::kIncomplete;
-      if (k < 0) return Parse::kBad;
+      if (k == 0) return incomplete(chunk_start);
+      if (k < 0) return fail(Parse::kBad);
       std::string sz = line.substr(0, line.find(';'));
       int64_t n = 0;
       if (strip(sz).empty()) n = 0;
-      else if (!py_int(sz, 16, &n) || n < 0) return Parse::kBad;
+      else if (!py_int(sz, 16, &n) || n < 0) return fail(Parse::kBad);
       if (n == 0) {
         k = take_line(in, pos, line);   // the line after the last chunk
-        if (k == 0) return Parse::kIncomplete;
-        if (k < 0) return Parse::kBad;
+        if (k == 0) return incomplete(chunk_start);
+        if (k < 0) return fail(Parse::kBad);
         break;
       }
-      total += n;
-      if (total > max_body) return Parse::kTooLarge;
-      if (in.size() - pos < static_cast<size_t>(n)) return Parse::kIncomplete;
-      spans.emplace_back(pos, static_cast<size_t>(n));
+      if (st.total + n > max_body) return fail(Parse::kTooLarge);
+      if (in.size() - pos < static_cast<size_t>(n)) return incomplete(chunk_start);
+      const size_t data = pos;
       pos += static_cast<size_t>(n);
       k = take_line(in, pos, line);
-      if (k == 0) return Parse::kIncomplete;
-      if (k < 0) return Parse::kBad;
+      if (k == 0) return incomplete(chunk_start);
+      if (k < 0) return fail(Parse::kBad);
+      st.total += n;   // the chunk is whole: counted once, kept relative to start
+      st.spans.emplace_back(data - start, static_cast<size_t>(n));
     }
-    r->body.reserve(static_cast<size_t>(total));
-    for (const auto& sp : spans) r->body.append(in, sp.first, sp.second);
-  } else {
+    r->body.reserve(static_cast<size_t>(st.total));
+    for (const auto& sp : st.spans) r->body.append(in, start + sp.first, sp.second);
+    st.active = false;
+    st.spans.clear();
+    r->end = pos;
+    return Parse::kDone;
+  }
+plain : {
+    r->body.clear();
     int64_t n = 0;
     auto cl = r->h.find("content-length");
     if (cl != r->h.end() && !cl->second.empty() && !py_int(cl->second, 10, &n)) return Parse::kBad;
@@ -810,7 +881,7 @@ bool process(IoThread& t, Conn* c) {
       return true;
     }
     Req r;
-    const Parse p = parse_request(c->in, c->in_off, s.cfg.max_body_bytes, &r);
+    const Parse p = parse_request(c->in, c->in_off, s.cfg.max_body_bytes, &r, &c->chunk);
     if (p == Parse::kIncomplete) {
       if (c->in_off > (1u << 16)) {   // keep the buffer from growing at its front
         c->in.erase(0, c->in_off);
@@ -840,6 +911,26 @@ bool process(IoThread& t, Conn* c) {
   return true;
 }
 
+void on_readable(IoThread& t, Conn* c);
+
+// the peer has shut its side and nothing is in flight: every complete request
+// has been dispatched (process stops only at a busy connection, an incomplete
+// request or the end of the buffer), so a partial request left is answered
+// 400 as the Python server's IncompleteReadError is, then the connection
+// closes once its answers are written
+void finish_at_eof(IoThread& t, Conn* c) {
+  if (!c->peer_eof || c->busy || c->fd < 0) return;
+  if (c->in_off < c->in.size() && !c->close_after) {
+    append_error(c->out, 400, "Bad Request");
+    t.srv->n_bad.fetch_add(1);
+  }
+  c->in.clear();
+  c->in_off = 0;
+  c->chunk.active = false;
+  c->close_after = true;
+  flush_out(t, c);
+}
+
 void on_done(IoThread& t, Done& d) {
   auto it = t.conns.find(d.conn);
   if (it == t.conns.end()) return;
@@ -860,17 +951,35 @@ void on_done(IoThread& t, Done& d) {
     t.conns.erase(it);
     return;
   }
-  if (flush_out(t, c)) process(t, c);
+  if (!flush_out(t, c) || !process(t, c) || c->fd < 0) return;
+  if (c->read_paused) {   // edge-triggered: the bytes left in the socket raise no new event
+    c->read_paused = false;
+    on_readable(t, c);
+    return;
+  }
+  finish_at_eof(t, c);
 }
 
 void on_readable(IoThread& t, Conn* c) {
   char buf[65536];
   size_t since = 0;   // bytes read since the buffer was last parsed
-  for (;;) {
+  size_t got = 0;     // bytes read in this wake-up
+  while (!c->peer_eof) {
+    // backpressure: a request in flight with kMaxPipelined bytes queued behind
+    // it stops the reading until its answer is out (on_done resumes it)
+    if (c->busy && c->in.size() - c->in_off >= kMaxPipelined) {
+      c->read_paused = true;
+      return;
+    }
+    if (got >= kReadBudget) {   // fairness: the thread's other connections first
+      t.again.push_back(c->id);
+      break;
+    }
     const ssize_t n = read(c->fd, buf, sizeof buf);
     if (n > 0) {
       c->in.append(buf, static_cast<size_t>(n));
       since += static_cast<size_t>(n);
+      got += static_cast<size_t>(n);
       // a sender that keeps the socket readable does not grow the buffer
       // unparsed: every MB the framing is checked (a bad line or a body over
       // the limit closes the connection now) and complete requests dispatched
@@ -883,21 +992,12 @@ void on_readable(IoThread& t, Conn* c) {
     }
     if (n < 0 && errno == EINTR) continue;
     if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
-    // EOF or error: what was complete is still answered (the Python
-    // server reads requests until the stream ends), then the connection closes
-    if (!c->busy && !process(t, c)) return;
-    if (c->fd >= 0) {
-      if (c->busy) {
-        c->close_after = true;   // answer the request in flight, then close
-      } else if (c->out_off >= c->out.size()) {
-        close_conn(t, c);
-      } else {
-        c->close_after = true;
-      }
-    }
-    return;
+    // EOF or error: every complete request is still answered, in order (the
+    // Python server reads requests until the stream ends), then it closes
+    c->peer_eof = true;
   }
-  process(t, c);
+  if (!c->busy && !process(t, c)) return;
+  if (c->fd >= 0) finish_at_eof(t, c);
 }
 
 // a connection joins thread t: registered in its epoll set, then read
@@ -952,8 +1052,10 @@ void io_main(IoThread* tp) {
   epoll_event evs[256];
   std::deque<Done> local;
   std::vector<int> fds;
+  std::vector<uint64_t> again;
   while (!s.stop.load()) {
-    const int n = epoll_wait(t.ep, evs, 256, 200);
+    const int n = epoll_wait(t.ep, evs, 256, t.again.empty() ? 200 : 0);
+    again.swap(t.again);   // read on, after this round's events (kReadBudget)
     for (int i = 0; i < n; ++i) {
       const uint64_t key = evs[i].data.u64;
       if (key == kListen) {
@@ -981,6 +1083,11 @@ void io_main(IoThread* tp) {
         if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) on_readable(t, c);
       }
     }
+    for (const uint64_t key : again) {
+      auto it = t.conns.find(key);
+      if (it != t.conns.end() && it->second->fd >= 0) on_readable(t, it->second.get());
+    }
+    again.clear();
   }
 }
 
@@ -1008,12 +1115,32 @@ void native_done(void* ctx, const kb_completion* c) {
 }
 
 // no new requests reach the route's batcher (removed from the table): send
-// what it holds to the model, wait for those requests' completions, then
-// detach the callback, after which the application may destroy the batcher
-void detach(RouteCtx* ctx) {
+// what it holds to the model and wait for those requests' completions, then
+// detach the callback, after which the application may destroy the batcher.
+// A completion writes into its connection's buffer, so the callback is never
+// detached while one is outstanding: after `timeout_s` (< 0: no limit) the
+// route stays attached (its context lives as long as the server, so late
+// completions still reach their connections) and false is returned
+bool detach(RouteCtx* ctx, double timeout_s) {
   kb_flush(ctx->batcher);
-  for (int i = 0; i < 400000 && ctx->inflight.load() > 0; ++i) usleep(50);
+  const auto t0 = std::chrono::steady_clock::now();
+  double warned = 0;
+  while (ctx->inflight.load() > 0) {
+    usleep(50);
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_s >= 0 && el >= timeout_s) {
+      fprintf(stderr, "kfhttp: %lld request(s) still on a retired route's batcher after %.0f s; "
+              "its callback stays attached\n", static_cast<long long>(ctx->inflight.load()), el);
+      return false;
+    }
+    if (el - warned >= 20) {
+      warned = el;
+      fprintf(stderr, "kfhttp: waiting for %lld request(s) on a batcher (%.0f s)\n",
+              static_cast<long long>(ctx->inflight.load()), el);
+    }
+  }
   kb_set_done_callback(ctx->batcher, nullptr, nullptr);
+  return true;
 }
 
 }  // namespace
@@ -1147,8 +1274,7 @@ int kh_remove_route(void* h, const char* model) {
     ctx = it->second.ctx;
     s.routes.erase(it);
   }
-  detach(ctx);
-  return 0;
+  return detach(ctx, 20.0) ? 0 : -2;
 }
 
 int kh_start(void* h) {
@@ -1225,14 +1351,15 @@ int kh_destroy(void* h) {
     if (t->th.joinable()) t->th.join();
   // requests still on a batcher write into their connection's buffer: every
   // route is detached (its completions arrive in the stopped threads' queues)
-  // before anything is freed
+  // before anything is freed, with no time limit (a completion
+  // after the connections are freed would write into freed memory)
   std::vector<RouteCtx*> live;
   {
     std::lock_guard<std::mutex> lk(s->rmu);
     for (auto& kv : s->routes) live.push_back(kv.second.ctx);
     s->routes.clear();
   }
-  for (RouteCtx* c : live) detach(c);
+  for (RouteCtx* c : live) detach(c, -1.0);
   for (auto& t : s->io) {
     for (const int fd : t->new_fds) close(fd);
     for (auto& kv : t->conns)

@@ -471,12 +471,34 @@ constexpr int kMaxHeapDepth = 8;              // deeper forests use the explicit
 constexpr size_t kLdsPerCu = 160 * 1024;      // gfx950
 constexpr size_t kFeatLdsMax = 64 * 1024;     // feature image budget per workgroup
 
-// Tuning knobs (read once): TI_HEAP_ROWS = rows per heap workgroup,
-// TI_HEAP_LDS_KB = LDS budget per heap workgroup (features + tree stage).
-int env_int(const char* name, int dflt) {
+// Environment knobs.  The layout / kernel A/B switches (TI_FORCE_LAYOUT,
+// TI_TX_TOP, TI_LX_ILP, ...) are developer knobs, read only when
+// TI_DEV_KNOBS=1: a serving worker that inherits a stray variable runs the
+// default kernels (the reference plugin's one knob is
+// nthread, python/xgbserver/xgbserver/model.py:38).  The operational settings
+// below are always read; they change speed or memory, never the kernel or the
+// results, and the per-forest ones are also ti_forest_set_option's.
+bool dev_knobs() {
+  const char* v = std::getenv("TI_DEV_KNOBS");
+  return v && std::atoi(v) == 1;
+}
+
+bool operational_knob(const char* name) {
+  static const char* const kOps[] = {"TI_CHUNK_MB", "TI_SHAP_TABLE_ROWS", "TI_SHAP_TABLE_MB"};
+  for (const char* k : kOps)
+    if (std::strcmp(k, name) == 0) return true;
+  return false;
+}
+
+const char* env_knob(const char* name) {
+  if (!operational_knob(name) && !dev_knobs()) return nullptr;
   const char* v = std::getenv(name);
-  if (!v || !*v) return dflt;
-  return std::atoi(v);
+  return v && *v ? v : nullptr;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = env_knob(name);
+  return v ? std::atoi(v) : dflt;
 }
 
 // Rows per tile (= threads per workgroup) for a feature image of F columns
@@ -666,6 +688,8 @@ struct ti_forest {
   int64_t shap_tab_len = 0;
   int64_t shap_tab_rows = env_int("TI_SHAP_TABLE_ROWS", 16384);
   int64_t shap_tab_mb = env_int("TI_SHAP_TABLE_MB", 1280);
+  // TI_OPT_HOST_REGISTER (developer default: $TI_HOST_REGISTER under TI_DEV_KNOBS)
+  std::atomic<int32_t> host_register{env_int("TI_HOST_REGISTER", 0) != 0 ? 1 : 0};
   double shap_tab_build_ms = 0.0;   // the last table build (slot's shap_table_kernel + upload)
   std::vector<ShapElem> h_elems;
   std::vector<double> h_path_leaf, h_shap_bias;
@@ -1636,10 +1660,7 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
     bmask16 = wmask16 | 2u;
   }
   const uint32_t zfb = (b16 && f->zero_rule) ? ti::kT16ZfBytes : 0u;
-  // per-lane progress (t16lane_predict_kernel, b16 only): no heap top,
-  // stages of at most kLaneTrees trees
-  const bool lane = b16 && env_int("TI_TX16_PERLANE", 0) != 0;
-  int D0 = lane ? 0 : env_int("TI_TX_TOP", b16 ? 8 : 6);
+  int D0 = env_int("TI_TX_TOP", b16 ? 8 : 6);
   // (the u16 bottom also runs without a top: D0 = 0, the root the only entry)
   D0 = std::max(b16 ? 0 : 1, std::min(D0, std::min(D, 10)));
   const int T = d->n_trees;
@@ -1728,9 +1749,7 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
   while (t0 < T) {
     int t1 = t0 + 1;
     while (t1 < T && off[t1 + 1] - off[t0] <= cap) ++t1;
-    if (lane) {
-      t1 = std::min(t1, t0 + ti::kLaneTrees);
-    } else if (t1 < T && t1 - t0 > ilp) {
+    if (t1 < T && t1 - t0 > ilp) {
       t1 = t0 + ((t1 - t0) / ilp) * ilp;
     }
     stages.push_back(t1);
@@ -1819,7 +1838,7 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
   f->lx_stage_cap = static_cast<int64_t>(cap);
   f->lx_ilp = ilp;
   f->hx_top = D0;
-  f->tx8 = lane ? 3 : b16 ? 2 : 1;
+  f->tx8 = b16 ? 2 : 1;
   f->tx16_mask = bmask16;
   f->layout = 9;
   return true;
@@ -2083,11 +2102,8 @@ KernelFn select_lexplicit(int xdt, int accum, int K, bool z, int ilp) {
 
 // Columns per pass of the record layouts' coalesced binning through the stage
 // area (rx_stage_bins): a multiple of 8 that fits `bytes` for R rows, at most
-// the features rounded up to 8; 0 (per-lane row loads) when fewer than 8 fit
-// or TI_BIN_TILED=0.
+// the features rounded up to 8; 0 (per-lane row loads) when fewer than 8 fit.
 int32_t bin_chunk_for(size_t bytes, int R, int xdt, int F) {
-  static const int tiled = env_int("TI_BIN_TILED", 1);
-  if (!tiled) return 0;
   const size_t per_col = static_cast<size_t>(R) * (xdt == TI_F64 ? 8 : 4);
   size_t c = (bytes / per_col) & ~size_t(7);
   c = std::min(c, static_cast<size_t>((F + 7) & ~7));
@@ -2113,13 +2129,6 @@ KernelFn select_t16explicit(int xdt, int accum, int K, bool z, int ilp) {   // l
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(12, K, true, z, true, ilp);
   if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(12, K, true, z, true, ilp);
   return ti::kernels_df(12, K, true, z, true, ilp);
-}
-
-KernelFn select_t16lane(int xdt, int accum, int K, bool z) {   // layout 9, u16, per-lane progress
-  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(13, K, true, z, true, 0);
-  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(13, K, true, z, true, 0);
-  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(13, K, true, z, true, 0);
-  return ti::kernels_df(13, K, true, z, true, 0);
 }
 
 KernelFn select_hexplicit(int xdt, int accum, int K, bool z, int ilp) {
@@ -2414,8 +2423,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.tx_vals = d.tx8_val;
     a.tx_ord = d.tx8_ord;
     a.bin_mask = f->tx16_mask;
-    KernelFn fn = f->tx8 == 3 ? select_t16lane(xdt, f->accum, f->K, f->zero_rule != 0)
-                : f->tx8 == 2 ? select_t16explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
+    KernelFn fn = f->tx8 == 2 ? select_t16explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
                 : f->tx8 ? select_t8explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
                          : select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp, rx.b8 != 0);
     int rc = ensure_lds_attr(d.device, fn);
@@ -2608,41 +2616,51 @@ int predict_pipelined(ti_forest* f, int slot, DeviceForest& d, const unsigned ch
   return rc ? rc : (r1 ? r1 : r2);
 }
 
+// A caller's host span page-locked for one call (hipHostRegister over its
+// page-rounded range) and unlocked when this goes out of scope.  Only a
+// registration this call made counts: pages that another registration already
+// holds (hipErrorHostMemoryAlreadyRegistered) may be unlocked by their owner
+// mid-DMA, so reg() reports failure and the caller takes the staging chunks.
+struct HostSpan {
+  void* p = nullptr;
+  bool mine = false;
+  bool reg(const void* base, size_t n, bool portable = false) {
+    const uintptr_t pg = 4096;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(base) & ~(pg - 1);
+    const uintptr_t hi = (reinterpret_cast<uintptr_t>(base) + n + pg - 1) & ~(pg - 1);
+    p = reinterpret_cast<void*>(lo);
+    const hipError_t e = hipHostRegister(p, hi - lo, portable ? hipHostRegisterPortable
+                                                                : hipHostRegisterDefault);
+    if (e == hipSuccess) {
+      mine = true;
+      return true;
+    }
+    (void)hipGetLastError();
+    return false;
+  }
+  ~HostSpan() {
+    if (mine) (void)hipHostUnregister(p);
+  }
+};
+
 // The caller's own buffers page-locked for the call (hipHostRegister), so
 // chunks go H2D straight from X and D2H straight into out, alternating two
-// lanes with no host copy and no host wait until the end (TI_HOST_REGISTER=1;
+// lanes with no host copy and no host wait until the end (TI_OPT_HOST_REGISTER;
 // A/B against the pinned-chunk pipeline, which copies every byte once on the
 // host).  Returns TI_ERR_UNSUPPORTED, having done nothing, when a buffer
 // cannot be registered; the caller then takes the pinned-chunk pipeline.
+// `pre`: the caller registered X and out already (the multi-device ti_predict
+// registers the whole batch once, before its shard threads start).
 int predict_registered(ti_forest* f, int slot, DeviceForest& d, const unsigned char* X, int xdt,
                        int64_t rows, int32_t cols, int64_t stride, int kind, unsigned char* out,
-                       int64_t ch) {
+                       int64_t ch, bool pre) {
   const size_t xs = dtype_size(xdt);
   const size_t os = dtype_size(output_dtype(f, kind)) * output_width(f, kind);
   const size_t x_row = static_cast<size_t>(stride) * xs;
   const size_t x_bytes = static_cast<size_t>((rows - 1) * stride + cols) * xs;
   const size_t o_bytes = static_cast<size_t>(rows) * os;
-  const uintptr_t pg = 4096;
-  struct Reg {
-    void* p = nullptr;
-    bool mine = false;
-    ~Reg() {
-      if (mine) (void)hipHostUnregister(p);
-    }
-  } rx, ro;
-  auto reg = [&](Reg& r, const void* base, size_t n) -> bool {
-    const uintptr_t lo = reinterpret_cast<uintptr_t>(base) & ~(pg - 1);
-    const uintptr_t hi = (reinterpret_cast<uintptr_t>(base) + n + pg - 1) & ~(pg - 1);
-    r.p = reinterpret_cast<void*>(lo);
-    const hipError_t e = hipHostRegister(r.p, hi - lo, hipHostRegisterDefault);
-    if (e == hipSuccess) {
-      r.mine = true;
-      return true;
-    }
-    (void)hipGetLastError();
-    return e == hipErrorHostMemoryAlreadyRegistered;
-  };
-  if (!reg(rx, X, x_bytes) || !reg(ro, out, o_bytes)) return TI_ERR_UNSUPPORTED;
+  HostSpan rx, ro;
+  if (!pre && (!rx.reg(X, x_bytes) || !ro.reg(out, o_bytes))) return TI_ERR_UNSUPPORTED;
   struct LaneSync {
     DeviceForest& d;
     ~LaneSync() {
@@ -2690,15 +2708,19 @@ int predict_registered(ti_forest* f, int slot, DeviceForest& d, const unsigned c
   return TI_OK;
 }
 
+// reg: 0 pinned staging chunks; 1 page-lock this shard's X and out for the
+// call (one device); 2 the caller page-locked the whole batch (multi-device)
 int predict_shard(ti_forest* f, int slot, DeviceForest& d, const unsigned char* X, int xdt,
-                  int64_t rows, int32_t cols, int64_t stride, int kind, unsigned char* out) {
+                  int64_t rows, int32_t cols, int64_t stride, int kind, unsigned char* out,
+                  int reg) {
   std::lock_guard<std::mutex> lk(d.mu);
   TI_HIP(hipSetDevice(d.device));
   {
     const int64_t ch = chunk_rows(static_cast<size_t>(stride) * dtype_size(xdt));
     if (rows > ch) {
-      if (env_int("TI_HOST_REGISTER", 0)) {
-        const int rc = predict_registered(f, slot, d, X, xdt, rows, cols, stride, kind, out, ch);
+      if (reg) {
+        const int rc = predict_registered(f, slot, d, X, xdt, rows, cols, stride, kind, out, ch,
+                                          reg == 2);
         if (rc != TI_ERR_UNSUPPORTED) return rc;
       }
       return predict_pipelined(f, slot, d, X, xdt, rows, cols, stride, kind, out, ch);
@@ -3272,7 +3294,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   // trees, the float explicit kernel for categorical splits;
   // TI_FORCE_LAYOUT=heap|explicit|rexplicit|lexplicit|hexplicit|texplicit
   // overrides (tests run every layout on the same forest)
-  const char* force = std::getenv("TI_FORCE_LAYOUT");
+  const char* force = env_knob("TI_FORCE_LAYOUT");
   std::string want = force ? force : "";
   bool use_heap = D <= kMaxHeapDepth;
   if (want == "heap" && D <= kMaxHeapDepth) use_heap = true;
@@ -3284,8 +3306,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
   // binned heap (rank-binned features, 4-byte nodes) for complete-able trees
   // without LightGBM zero-missing or categorical splits; TI_FORCE_LAYOUT=heap
   // keeps the float-compare heap kernel
-  bool use_bheap = use_heap && want != "heap" && f->zero_rule == 0 && D >= 1 &&
-                   env_int("TI_NO_BHEAP", 0) == 0;
+  bool use_bheap = use_heap && want != "heap" && f->zero_rule == 0 && D >= 1;
   if (use_bheap) {
     bool ok;
     if (f->accum == TI_F64)
@@ -3330,8 +3351,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
     // record explicit slots (layout 6) unless a categorical split needs raw
     // values or another explicit kernel is forced
     bool rx_ok = false;
-    if (!f->has_cat && want != "explicit" &&
-        env_int("TI_NO_REXPLICIT", 0) == 0) {
+    if (!f->has_cat && want != "explicit") {
       std::vector<uint32_t> slot_of;
       rx_ok = plan_rx_slots(desc, f.get(), &slot_of);
       auto pack_views = [&](bool b8) {
@@ -3344,8 +3364,7 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
       // u8 bins where every feature's thresholds fit them and layout 9 takes
       // the forest (only layout 9 reads u8 images; TI_RX_B8=0 keeps u16)
       const bool try8 = rx_ok && env_int("TI_RX_B8", 1) != 0 &&
-                        (want.empty() || want == "texplicit") &&
-                        env_int("TI_NO_TEXPLICIT", 0) == 0;
+                        (want.empty() || want == "texplicit");
       bool b8 = try8 && pack_views(true) &&
                 (plan_tx8(desc, f.get(), slot_of, D) || plan_tx(desc, f.get(), slot_of, D));
       if (!b8 && rx_ok) rx_ok = pack_views(false);
@@ -3360,19 +3379,19 @@ int ti_forest_create(const ti_forest_desc* desc, const int32_t* devices, int32_t
         if (force_ilp > 0) f->rx_ilp = force_ilp >= 16 ? 16 : force_ilp >= 8 ? 8 : 4;
         // small trees: a heap top and the rest staged in LDS (layout 9; C3
         // 1M rows 5.83 vs 6.15 ms for layout 7), or all records staged
-        // (layout 7, forced or TI_NO_TEXPLICIT=1); deep trees too large for a
+        // (layout 7, forced, or when layout 9 does not fit); deep trees too large for a
         // stage: heap tops in LDS, the rest gathered (layout 8)
         const bool auto_ok = want != "rexplicit" && want != "hexplicit" && want != "lexplicit";
         if (b8) {
           f->layout = 9;   // u8 bins (planned above)
-        } else if ((want == "texplicit" || (auto_ok && env_int("TI_NO_TEXPLICIT", 0) == 0)) &&
+        } else if ((want == "texplicit" || auto_ok) &&
                    (plan_tx8(desc, f.get(), slot_of, D, true) || plan_tx(desc, f.get(), slot_of, D))) {
           // layout 9 (the compact u16 bottom where it fits, else records)
-        } else if ((want == "lexplicit" || auto_ok) && env_int("TI_NO_LEXPLICIT", 0) == 0 &&
+        } else if ((want == "lexplicit" || auto_ok) &&
                    plan_lx_stages(f.get(), f->T)) {
           f->layout = 7;
         } else if (want == "hexplicit" ||
-                   (want != "rexplicit" && D >= kHxMinDepth && env_int("TI_NO_HEXPLICIT", 0) == 0)) {
+                   (want != "rexplicit" && D >= kHxMinDepth)) {
           plan_htop(desc, f.get(), slot_of, D);
         }
       } else {
@@ -3485,6 +3504,10 @@ int ti_forest_set_option(ti_forest* f, int32_t option, int64_t value) {
       if (value < 0) return fail(TI_ERR_INVALID, "TI_OPT_SHAP_TABLE_MB must be >= 0");
       f->shap_tab_mb = value;
       return TI_OK;
+    case TI_OPT_HOST_REGISTER:
+      if (value != 0 && value != 1) return fail(TI_ERR_INVALID, "TI_OPT_HOST_REGISTER must be 0 or 1");
+      f->host_register.store(static_cast<int32_t>(value));
+      return TI_OK;
     default:
       return fail(TI_ERR_INVALID, "unknown option " + std::to_string(option));
   }
@@ -3527,7 +3550,22 @@ int ti_predict(ti_forest* f, const void* X, int32_t xdt, int64_t rows, int32_t c
   const int64_t per = (rows + nd - 1) / nd;
   const unsigned char* xb = static_cast<const unsigned char*>(X);
   unsigned char* ob = static_cast<unsigned char*>(out);
-  if (nd == 1) return predict_shard(f, 0, *bf->devs[0], xb, xdt, rows, cols, stride, kind, ob);
+  const bool hreg = bf->host_register.load() != 0;
+  if (nd == 1)
+    return predict_shard(f, 0, *bf->devs[0], xb, xdt, rows, cols, stride, kind, ob, hreg ? 1 : 0);
+  // registered buffers (TI_OPT_HOST_REGISTER) with several devices: the whole
+  // X and output are page-locked once here, before the shard threads start,
+  // and unlocked after they join (shard threads registering their
+  // own page-rounded slices shared boundary pages, and one thread's unregister
+  // could unlock pages under another's in-flight DMA).  If either span cannot
+  // be registered every shard takes the pinned staging chunks.
+  HostSpan all_x, all_o;
+  int reg_mode = 0;
+  if (hreg && per > chunk_rows(static_cast<size_t>(stride) * xs)) {
+    const size_t x_bytes = static_cast<size_t>((rows - 1) * stride + cols) * xs;
+    if (all_x.reg(xb, x_bytes, true) && all_o.reg(ob, static_cast<size_t>(rows) * os, true))
+      reg_mode = 2;
+  }
   std::vector<int> rcs(nd, TI_OK);
   std::vector<std::string> errs(nd);
   std::vector<std::thread> th;
@@ -3537,11 +3575,11 @@ int ti_predict(ti_forest* f, const void* X, int32_t xdt, int64_t rows, int32_t c
     if (r0 >= r1) break;
     th.emplace_back([&, i, r0, r1]() {
       rcs[i] = predict_shard(f, i, *bf->devs[i], xb + r0 * stride * xs, xdt, r1 - r0, cols, stride,
-                             kind, ob + r0 * os);
+                             kind, ob + r0 * os, reg_mode);
       if (rcs[i]) errs[i] = g_last_error;
     });
   }
-  for (auto& t : th) t.join();
+  for (auto& t : th) t.join();   // before all_x / all_o unregister
   for (int i = 0; i < nd; ++i)
     if (rcs[i]) return fail(rcs[i], "device slot " + std::to_string(i) + ": " + errs[i]);
   return TI_OK;

@@ -41,12 +41,6 @@ KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
            : pf == 7 ? t8explicit_predict_kernel<XT, ACC, KMAX, false, 7>
                      : t8explicit_predict_kernel<XT, ACC, KMAX, false, 4>;
   }
-  if (layout == 13) {   // compact u16 image, per-lane progress (TI_TX16_PERLANE)
-    if constexpr (sizeof(ACC) == 8) {
-      if (z) return t16lane_predict_kernel<XT, ACC, KMAX, true, kLaneSlots, kLaneTurns>;
-    }
-    return t16lane_predict_kernel<XT, ACC, KMAX, false, kLaneSlots, kLaneTurns>;
-  }
   if (layout == 12) {   // layout 9 with the compact u16 bottom; pf carries the tree ILP
     if constexpr (sizeof(ACC) == 8) {
       if (z) return pf >= 8 ? t16explicit_predict_kernel<XT, ACC, KMAX, true, 8>

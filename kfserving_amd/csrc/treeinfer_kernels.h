@@ -2323,180 +2323,4 @@ __global__ void __launch_bounds__(512) t16explicit_predict_kernel(const KArgs a)
   finish_row<ACC, KMAX>(acc, a, row);
 }
 
-// ---- per-lane progress over the compact u16 image (TI_TX16_PERLANE=1) ------
-// VERDICT r4 asked for this walk to be built and measured.  The image is
-// plan_tx16's with no heap top (D0 = 0: the root is position 0), stages of at
-// most C x M trees.  Each lane keeps C slots; slot c walks the stage's trees
-// c, c + C, c + 2C, ... one after the other, so a slot whose tree reached a
-// leaf goes on to its next tree while the other slots and lanes are still
-// inside theirs (no group waits for its deepest path).  Everything is
-// branch-free selects on per-lane state: a completed tree's leaf position is
-// written into the slot's j-th register (static index j, compared with the
-// slot's count k), the slot's base and position-table offset move to the
-// next tree (selects over the slot's M trees' uniform values), and its node
-// word becomes kT16Enter -- an even self-looping leaf word with pair index 0,
-// whose next step reads the new tree's pair 0 (root, pad) and goes left to
-// the root.  The loop ends when no slot of any lane has a tree left.  Leaf
-// values are added after the stage in tree order (one stage late, as
-// t8_stage's groups), so sums keep the library's order.
-constexpr uint32_t kT16Enter = 0xFFFF0001u;   // rank 0xFFFF, NaN-left, pair 0, bin offset 0
-constexpr int kLaneSlots = 4, kLaneTurns = 3;   // C slots a lane, M trees a slot
-constexpr int kLaneTrees = kLaneSlots * kLaneTurns;
-
-template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int C, int M>
-__device__ __forceinline__ void t16_lane_stage(const KArgs& a, ACC (&acc)[KMAX], int t0, int t1,
-                                               uint32_t sbase, uint32_t lane_off, int64_t row,
-                                               bool live, ACC (&pend)[C * M], int (&pend_t)[C * M]) {
-  rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
-  rx_cu32* tx_pos = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.tx_pos));
-  const uint32_t zfb = ZERO ? kT16ZfBytes : 0u;
-  const uint32_t skip = 8u + zfb;                   // the 8-byte top, the zero-flip bits
-  const uint32_t bmask = a.bin_mask;
-  const int G = t1 - t0;                            // <= C * M (plan_tx16)
-  uint32_t Bs[C][M], Ps[C][M];                      // per slot and turn: bottom base, position offset
-  int nt[C];                                        // trees of each slot
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    nt[c] = 0;
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-      const int q = c + C * j;
-      const int t = t0 + (q < G ? q : G - 1);
-      Bs[c][j] = sbase + tx_off[t] + skip;
-      Ps[c][j] = tx_pos[t];
-      nt[c] += q < G ? 1 : 0;
-    }
-  }
-  uint32_t x[C], base[C], pb[C], k[C], p[C], li[C][M];
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    x[c] = kT16Enter;
-    base[c] = Bs[c][0];
-    pb[c] = Ps[c][0];
-    k[c] = 0u;
-    p[c] = 1u;   // the entry word's position: the root's pad (zero-flip 0)
-#pragma unroll
-    for (int j = 0; j < M; ++j) li[c][j] = 0u;
-  }
-  for (;;) {
-    bool more = false;
-#pragma unroll
-    for (int c = 0; c < C; ++c) more |= k[c] < (uint32_t)nt[c];
-    if (__ballot(more) == 0) break;   // every slot of every lane walked all its trees
-    uint32_t b[C], zb[C];
-    rx_u2_t pr[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      b[c] = lds_u16((x[c] & bmask) | lane_off);
-      pr[c] = lx_rec(base[c] + ((x[c] & 0x3FCu) << 1));
-      if (SLOW && ZERO) zb[c] = lds_u8(base[c] - zfb + (p[c] >> 3));
-    }
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      if (!SLOW) {
-        asm("v_cmp_lt_u32_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:WORD_0\n\t"
-            "v_cndmask_b32 %0, %2, %3, vcc"
-            : "+v"(x[c]) : "v"(b[c]), "v"(pr[c].x), "v"(pr[c].y) : "vcc");
-      } else {
-        const bool zf = ZERO && ((zb[c] >> (p[c] & 7u)) & 1u) != 0u;
-        const bool right = t16_right_slow<ZERO>(x[c], b[c] & 0xFFFFu, zf);
-        if (ZERO) p[c] = ((x[c] >> 1) & 0x1FEu) + (right ? 1u : 0u);
-        x[c] = right ? pr[c].y : pr[c].x;
-      }
-      // a leaf reached (not the entry word, which the step has just left):
-      // record it, move the slot to its next tree
-      const bool done = (x[c] + 0x10000u) < 0x20000u && k[c] < (uint32_t)nt[c];
-      const uint32_t pos = pb[c] + ((x[c] >> 1) & 0x1FEu) + ((x[c] >> 16) == 0u ? 1u : 0u);
-#pragma unroll
-      for (int j = 0; j < M; ++j) li[c][j] = (done && k[c] == (uint32_t)j) ? pos : li[c][j];
-      k[c] += done ? 1u : 0u;
-      uint32_t nb = Bs[c][0], np = Ps[c][0];
-#pragma unroll
-      for (int j = 1; j < M; ++j) {
-        nb = k[c] == (uint32_t)j ? Bs[c][j] : nb;
-        np = k[c] == (uint32_t)j ? Ps[c][j] : np;
-      }
-      base[c] = done ? nb : base[c];
-      pb[c] = done ? np : pb[c];
-      x[c] = done ? kT16Enter : x[c];
-      if (SLOW && ZERO) p[c] = done ? 1u : p[c];
-    }
-  }
-  if (VIS) {
-    t8_flush<ACC, KMAX, C * M>(a, acc, pend, pend_t);   // the previous stage's leaves
-#pragma unroll
-    for (int q = 0; q < C * M; ++q) {
-      pend[q] = static_cast<const ACC*>(a.tx_vals)[li[q % C][q / C]];
-      pend_t[q] = q < G ? t0 + q : -1;
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < C * M; ++q) {
-      const int t = t0 + q;
-      if (q < G) {
-        const int64_t lf = a.leaf_base[t] + (int64_t)a.tx_ord[li[q % C][q / C]];
-        if (a.kind == TI_OUTPUT_LEAF) {
-          if (live) static_cast<int32_t*>(a.out)[row * a.n_trees + t] = a.exp_leaf_ids[lf];
-        } else {
-          add_leaf<ACC, KMAX>(acc, static_cast<const ACC*>(a.leaves) + lf * a.leaf_width, 0,
-                              a.leaf_width, a.tree_group[t]);
-        }
-      }
-    }
-  }
-}
-
-template <typename XT, typename ACC, int KMAX, bool ZERO, int C, int M>
-__global__ void __launch_bounds__(512) t16lane_predict_kernel(const KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int PF = 8;   // = kLxPf (host)
-  const int R = blockDim.x;
-  const int tid = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * R;
-  const int64_t row = row0 + tid;
-  const bool live = row < a.n_rows;
-  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
-  u32x4* stage = reinterpret_cast<u32x4*>(smem + a.stage_off);
-  const uint32_t lane_off = (uint32_t)tid * 4u;
-  rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
-  rx_cu32* sst = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.stage_start));
-  const unsigned char* img = a.trees;
-  const int NS = a.n_stages;
-  auto lo_of = [&](int s) { return tx_off[sst[s]]; };
-  auto n16_of = [&](int s) { return (int)((tx_off[sst[s + 1]] - tx_off[sst[s]]) >> 4); };
-  u32x4 pf[PF];
-  prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(0)), n16_of(0), tid, R);
-  const bool slow = rx_stage_bins<XT, ZERO, false, false>(flag, a, row0, R, tid, stage);
-  const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
-  ACC acc[KMAX];
-  init_acc(acc, a);
-  ACC pend[C * M];
-  int pend_t[C * M];
-#pragma unroll
-  for (int q = 0; q < C * M; ++q) {
-    pend[q] = ACC(0);
-    pend_t[q] = -1;
-  }
-  for (int s = 0; s < NS; ++s) {
-    const int t0 = (int)sst[s], t1 = (int)sst[s + 1];
-    const uint32_t lo = lo_of(s);
-    __syncthreads();
-    commit_u<PF>(pf, stage, n16_of(s), tid, R);
-    __syncthreads();
-    const int sn = s + 1 < NS ? s + 1 : s;
-    prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(sn)), n16_of(sn), tid, R);
-    const uint32_t sbase = (uint32_t)a.stage_off - lo;
-    if (slow) {
-      if (vis) t16_lane_stage<ACC, KMAX, ZERO, true, true, C, M>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
-      else t16_lane_stage<ACC, KMAX, ZERO, true, false, C, M>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
-    } else {
-      if (vis) t16_lane_stage<ACC, KMAX, ZERO, false, true, C, M>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
-      else t16_lane_stage<ACC, KMAX, ZERO, false, false, C, M>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t);
-    }
-  }
-  if (vis) t8_flush<ACC, KMAX, C * M>(a, acc, pend, pend_t);
-  if (!live || a.kind == TI_OUTPUT_LEAF) return;
-  finish_row<ACC, KMAX>(acc, a, row);
-}
-
 }  // namespace ti

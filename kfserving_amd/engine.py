@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
 # ti_forest_set_option options (include/treeinfer.h)
 OPT_SHAP_TABLE_ROWS = 1
 OPT_SHAP_TABLE_MB = 2
+OPT_HOST_REGISTER = 3
 
 
 class TreeInferError(RuntimeError):
@@ -244,7 +245,7 @@ class DeviceForest:
 
     def set_option(self, option: int, value: int) -> None:
         """ti_forest_set_option: speed knobs that never change results
-        (OPT_SHAP_TABLE_ROWS, OPT_SHAP_TABLE_MB)."""
+        (OPT_SHAP_TABLE_ROWS, OPT_SHAP_TABLE_MB, OPT_HOST_REGISTER)."""
         _check(self._lib, self._lib.ti_forest_set_option(self._handle, option, int(value)))
 
     def output_shape(self, kind: int, n_rows: int):

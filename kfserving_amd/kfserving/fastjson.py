@@ -13,8 +13,10 @@ from typing import Optional
 
 import numpy as np
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
-                         "libkfserve.so")
+# KFSERVE_LIB: another build of the same library, e.g. the AddressSanitizer
+# build (__graft_entry__.build_host(asan=True), tests/test_asan_fuzz.py)
+_LIB_PATH = os.environ.get("KFSERVE_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libkfserve.so")
 _lib = None
 _lock = threading.Lock()
 

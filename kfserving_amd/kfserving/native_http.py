@@ -188,8 +188,7 @@ class NativeFrontEnd:
     def _register(self, name, spec) -> None:
         h, F, w, e, tr, labels, names = spec
         if name in self.routes:
-            self._lib.kh_remove_route(self._h, name.encode())
-            del self.routes[name]
+            self._remove_route(name)
         if names is not None:
             blob, offs = _blob(names)
             rc = self._lib.kh_add_v1_inputs_predict(self._h, name.encode(), h, F, w, e, blob, offs)
@@ -201,6 +200,13 @@ class NativeFrontEnd:
             rc = self._lib.kh_add_v1_predict(self._h, name.encode(), h, F, w, e, tr, blob, offs, n)
         if rc == 0:
             self.routes[name] = h
+
+    def _remove_route(self, key: str) -> None:
+        rc = self._lib.kh_remove_route(self._h, key.encode())
+        if rc == -2:   # requests still on the batcher after 20 s: it stays attached
+            logging.warning("native route %s retired with requests still in flight; "
+                            "their answers follow when the batcher drains", key)
+        del self.routes[key]
 
     def _on_batcher(self, event: str, name: str, kind: str, batcher) -> None:
         if self._h is None:
@@ -216,8 +222,7 @@ class NativeFrontEnd:
         if event == "retire" and name in self.routes:
             # detach before the batcher stops: kh_remove_route returns once the
             # requests already on it are answered
-            self._lib.kh_remove_route(self._h, name.encode())
-            del self.routes[name]
+            self._remove_route(name)
         elif event == "create":
             if route_spec_static(self.app, model) and not self.routes.get(name):
                 spec = _spec_of(batcher, model)
@@ -232,8 +237,7 @@ class NativeFrontEnd:
         the first such request (route key "v2:<name>")."""
         key = "v2:" + name
         if event == "retire" and key in self.routes:
-            self._lib.kh_remove_route(self._h, key.encode())
-            del self.routes[key]
+            self._remove_route(key)
         elif event == "create" and key not in self.routes:
             model = batcher.model
             tr = getattr(model, "native_v2_transform", None)

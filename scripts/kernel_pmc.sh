@@ -13,6 +13,8 @@ WL=$2
 shift 2
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# A/B knobs passed in the environment (TI_TX16=0 ...) need the developer gate
+export TI_DEV_KNOBS=${TI_DEV_KNOBS:-1}
 run() {  # name rocprof-args...
   local name=$1; shift
   (cd /tmp && timeout -k 10 150 rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv -- python3 "$ROOT/scripts/kernel_workload.py" --workload "$WL" "${ARGS[@]}") > "$OUT/$name.log" 2>&1

@@ -17,6 +17,12 @@ try:
 except ImportError:
     pass
 
+# the tests exercise every layout and A/B variant through libtreeinfer's
+# developer knobs (TI_FORCE_LAYOUT, TI_TX_TOP, ...), which the library reads
+# only under TI_DEV_KNOBS=1 (treeinfer.hip env_knob); tests/test_gpu_knob_gate.py
+# checks that without it they change nothing
+os.environ.setdefault("TI_DEV_KNOBS", "1")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP library)")

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from kfserving_amd.engine import DeviceForest
+from kfserving_amd.engine import OPT_HOST_REGISTER, DeviceForest
 from kfserving_amd.formats.xgboost_format import forest_from_raw_trees, synthetic_complete_trees
 from kfserving_amd.forest import OUT_LEAF, OUT_MARGIN, OUT_PREDICT, TI_F32
 from oracle import port
@@ -55,10 +55,11 @@ def test_chunked_host_predict_bit_exact(small_chunks):
 
 
 @pytest.mark.parametrize("strided", [False, True])
-def test_registered_host_predict_bit_exact(small_chunks, strided, monkeypatch):
-    """TI_HOST_REGISTER=1: the caller's X and out page-locked for the call,
-    chunks copied straight from / into them (predict_registered), the same
-    bits as the pinned-chunk pipeline; a row stride and a ragged last chunk."""
+def test_registered_host_predict_bit_exact(small_chunks, strided):
+    """TI_OPT_HOST_REGISTER=1: the caller's X and out page-locked for the
+    call, chunks copied straight from / into them (predict_registered), the
+    same bits as the pinned-chunk pipeline; a row stride and a ragged last
+    chunk."""
     trees, ti = synthetic_complete_trees(100, 8, 28, seed=4)
     f = forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic")
     dev = DeviceForest(f, [0])
@@ -66,7 +67,7 @@ def test_registered_host_predict_bit_exact(small_chunks, strided, monkeypatch):
     W = np.random.default_rng(7).standard_normal((rows, 32 if strided else 28)).astype(np.float32)
     X = W[:, :28]
     want = port.xgb_predict(trees, ti, 1, 0.0, 28, np.ascontiguousarray(X))[:, 0]
-    monkeypatch.setenv("TI_HOST_REGISTER", "1")
+    dev.set_option(OPT_HOST_REGISTER, 1)
     lib, ptr = dev._lib, lambda a: a.ctypes.data
     out = np.empty(rows, dtype=np.float32)
     rc = lib.ti_predict(dev._handle, ptr(W), TI_F32, rows, 28, W.shape[1], OUT_MARGIN, ptr(out), rows)
@@ -74,5 +75,35 @@ def test_registered_host_predict_bit_exact(small_chunks, strided, monkeypatch):
     assert np.array_equal(out, want)
     assert np.array_equal(dev.predict(np.ascontiguousarray(X), OUT_MARGIN), want)   # reused lanes
     leaf = dev.predict(np.ascontiguousarray(X), OUT_LEAF)
-    monkeypatch.setenv("TI_HOST_REGISTER", "0")
+    dev.set_option(OPT_HOST_REGISTER, 0)
     assert np.array_equal(leaf, dev.predict(np.ascontiguousarray(X), OUT_LEAF))
+
+
+def test_registered_host_predict_multi_device_and_already_registered(small_chunks):
+    """with several device slots the whole batch is page-locked
+    once before the shard threads start (slices sharing boundary pages used
+    to register and unregister them per thread); a buffer whose pages are
+    already registered by someone else is not used for direct DMA (the
+    pinned staging chunks take it).  Bit-exact against the C port both ways."""
+    trees, ti = synthetic_complete_trees(60, 8, 28, seed=8)
+    f = forest_from_raw_trees(trees, ti, 28, 0, 0.0, "binary:logistic")
+    dev = DeviceForest(f, [0, 0, 0])           # three slots: 3 shard threads
+    dev.set_option(OPT_HOST_REGISTER, 1)
+    rows = 61_111                              # 20,371 a slot: > 2 chunks each, ragged
+    X = np.random.default_rng(9).standard_normal((rows, 28)).astype(np.float32)
+    want = port.xgb_predict(trees, ti, 1, 0.0, 28, X)[:, 0]
+    for _ in range(2):
+        assert np.array_equal(dev.predict(X, OUT_MARGIN), want)
+    # X registered by another owner for the duration: the call must not rely
+    # on (or unregister) those pages
+    cudart = torch.cuda.cudart()
+    assert int(cudart.cudaHostRegister(X.ctypes.data, X.nbytes, 0)) == 0
+    try:
+        assert np.array_equal(dev.predict(X, OUT_MARGIN), want)
+        one = DeviceForest(f, [0])
+        one.set_option(OPT_HOST_REGISTER, 1)
+        assert np.array_equal(one.predict(X, OUT_MARGIN), want)
+        one.close()
+    finally:
+        assert int(cudart.cudaHostUnregister(X.ctypes.data)) == 0
+    dev.close()
