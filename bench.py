@@ -146,6 +146,9 @@ def parse_args(argv=None):
                         "exceeds the 256 MB Infinity Cache)")
     p.add_argument("--host-rows", type=int, default=8_000_000,
                    help="rows of the host-to-host (PCIe-inclusive) C2 leg (0 = skip)")
+    p.add_argument("--host-rows-configs", type=int, default=8_000_000,
+                   help="rows of the host-to-host (PCIe-inclusive) legs of the config "
+                        "workloads c3 / c3_f64 / c3_maxbin / c4 (rank 0; 0 = skip)")
     p.add_argument("--c5-http-qps", default="20000,100000,200000",
                    help="C5 over HTTP: offered req/s PER GPU of the points (x N for the node; "
                         "empty: skip); rank 0, after the GPU legs, a server of one worker per GPU")
@@ -816,13 +819,40 @@ def pool_latency(mine: dict, world: int, rank: int, device):
     return out
 
 
-def host_to_host(dev, X_host, rows, reps=3):
-    """C2 through ti_predict from pageable host memory to host memory (the
-    path the plugins take): chunks of TI_CHUNK_MB (64) MB alternate between two
-    streams, so H2D, kernel and D2H of neighbouring chunks overlap (DESIGN.md
-    5).  PCIe-inclusive; not the headline value."""
+_H2D = {}
+
+
+def pinned_h2d_GBps(device) -> float:
+    """Pinned host -> device copy rate of this box (1 GiB, best of 3), the
+    bound a host-buffer predict's input stream meets; measured once."""
+    if device in _H2D:
+        return _H2D[device]
+    import torch
+    n = 1 << 30
+    src = torch.empty(n, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(n, dtype=torch.uint8, device=device)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    best = 0.0
+    for _ in range(3):
+        t0 = time.perf_counter()
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, n / (time.perf_counter() - t0) / 1e9)
+    del src, dst
+    _H2D[device] = best
+    return best
+
+
+def host_to_host(dev, X_host, rows, reps=3, device="cuda"):
+    """A workload through ti_predict from pageable host memory to host memory
+    (the path the plugins take): chunks of TI_CHUNK_MB (64) MB alternate
+    between two streams, so H2D, kernel and D2H of neighbouring chunks overlap
+    (DESIGN.md 5).  PCIe-inclusive; never the headline value.  Beside the rate:
+    the input bytes a row, the box's pinned H2D rate and the rate that alone
+    would allow (`pcie_bound_rows_per_s`), and the fraction reached."""
     from kfserving_amd.forest import OUT_PREDICT
-    Xb = np.tile(X_host, (max(1, rows // X_host.shape[0]), 1))
+    Xb = np.tile(X_host, (max(1, -(-rows // X_host.shape[0])), 1))[:max(rows, 1)]
     dev.predict(Xb[:4096], OUT_PREDICT)
     times = []
     for _ in range(reps):
@@ -830,10 +860,18 @@ def host_to_host(dev, X_host, rows, reps=3):
         dev.predict(Xb, OUT_PREDICT)
         times.append(time.perf_counter() - t0)
     t = min(times)
-    return {"rows": Xb.shape[0], "chunk_mb": int(os.environ.get("TI_CHUNK_MB", "64")),
-            "rows_per_s": Xb.shape[0] / t, "ms": t * 1e3, "input_GBps": Xb.nbytes / t / 1e9,
-            "reps": reps, "path": "pageable numpy -> pinned chunks -> H2D -> kernel -> D2H -> "
-                                  "numpy, two streams"}
+    row_b = Xb.nbytes / Xb.shape[0]
+    res = {"rows": Xb.shape[0], "dtype": str(Xb.dtype), "bytes_per_row_in": row_b,
+           "chunk_mb": int(os.environ.get("TI_CHUNK_MB", "64")),
+           "rows_per_s": Xb.shape[0] / t, "ms": t * 1e3, "input_GBps": Xb.nbytes / t / 1e9,
+           "reps": reps, "path": "pageable numpy -> pinned chunks -> H2D -> kernel -> D2H -> "
+                                 "numpy, two streams"}
+    if device != "cpu":
+        h2d = pinned_h2d_GBps(device)
+        res.update(h2d_pinned_GBps=h2d, pcie_bound_rows_per_s=h2d * 1e9 / row_b,
+                   frac_of_pcie_bound=res["input_GBps"] / h2d)
+    del Xb
+    return res
 
 
 # ------------------------------------------------------------ other configs
@@ -917,7 +955,7 @@ def c4_forest():
 
 def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_sync,
                make_engine, cpu_fn=None, pmc_workload=None, pmc_path=None, dtype="float32",
-               cpu_cap=2_000_000):
+               cpu_cap=2_000_000, host_leg=False):
     """Strong scaling: this rank's block of the batch, K steps, max-over-ranks wall.
     The CPU baseline is not timed here: rank 0 keeps a host sample of its
     block (at most cpu_cap rows) and run() times it at the end."""
@@ -956,6 +994,14 @@ def run_config(forest, n_feat, total_rows, seed, args, world, rank, device, dev_
             # timed later (run: after every rank's GPU legs, on the full host):
             # keep a host copy of this rank's block, up to the sample cap
             res["_cpu"] = (cpu_fn, X[:min(rows, cpu_cap)].cpu().numpy())
+        if host_leg and args.host_rows_configs > 0 and hasattr(eng, "predict"):
+            # the plugins' real path: pageable numpy of
+            # the config's dtype -> ti_predict's pinned chunks -> H2D ->
+            # kernel -> D2H -> numpy (lgbserver hands float64 DataFrames,
+            # lgbserver/model.py:46-51; sklearnserver float32 after
+            # check_array, sklearnserver/model.py:46-51)
+            Xh = X[:min(rows, 1_000_000)].cpu().numpy()
+            res["_host_pipeline"] = host_to_host(eng, Xh, args.host_rows_configs, device=device)
     del X, out
     eng.close()
     if device != "cpu":
@@ -1217,7 +1263,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
 
     host_pipeline = None
     if args.host_rows > 0 and rank == 0 and device != "cpu":
-        host_pipeline = host_to_host(dev, X_host, args.host_rows)
+        host_pipeline = host_to_host(dev, X_host, args.host_rows, device=device)
 
     configs = {}
     for name in [c.strip() for c in args.configs.split(",") if c.strip()]:
@@ -1226,7 +1272,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             dt = "float64" if name == "c3_f64" else "float32"
             r = run_config(f3, 100, args.rows3, 3, args, world, rank, device, dev_sync,
                            make_engine, c3_cpu(t3, args.cpu_seconds / 2, dt), name,
-                           pmc_path(name), dt)
+                           pmc_path(name), dt, host_leg=name != "c3_maxbin")
             if r is not None:
                 r.update(config=f"C3 LightGBM leaf-wise 1000 trees x 255 leaves, 100 features, "
                                 f"{dt} input, float64 sigmoid of the raw score", model=src)
@@ -1241,7 +1287,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             f4, raw4, src = c4_forest()
             r = run_config(f4, 64, args.rows4, 2, args, world, rank, device, dev_sync,
                            make_engine, c4_cpu(raw4, args.cpu_seconds / 2), "c4",
-                           pmc_path("c4"), cpu_cap=10_000_000)
+                           pmc_path("c4"), cpu_cap=10_000_000, host_leg=True)
             if r is not None:
                 r.update(config="C4 sklearn RandomForestRegressor 200 trees max_depth 16, "
                                 "64 features, float32 input, float64 mean", model=src)
@@ -1275,9 +1321,12 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
                     r.update(got)               # C4: the library and the port
                 else:
                     r["cpu_baseline"] = got
-    for r in configs.values():
+    host_configs = {}
+    for name, r in configs.items():
         if r is not None:
             r.pop("_cpu", None)
+            if "_host_pipeline" in r:
+                host_configs["host_pipeline_" + name] = r.pop("_host_pipeline")
     line = None
     if rank == 0:
         line = {
@@ -1316,6 +1365,7 @@ def run(args, device="cuda", backend="nccl", make_engine=None):
             "c5_http_v2": c5_http_v2,
         }
         line.update(configs)
+        line.update(host_configs)
     return line
 
 

@@ -39,6 +39,11 @@ class StubEngine:
     def transform_device(self, margin_ptr, n_rows, out_ptr, out_len, slot=0, stream=0):
         pass
 
+    def predict(self, X, kind=0):
+        """Host-buffer predict (the host_pipeline legs): zeros."""
+        import numpy as np
+        return np.zeros(np.asarray(X).shape[0], dtype=np.float32)
+
     def info(self):
         return {"layout": 3}
 
@@ -52,7 +57,8 @@ def _worker(rank, world, port, q):
     import bench
     args = bench.parse_args(["--steps", "5", "--warmup", "1", "--rows", "4096",
                              "--configs", "c3", "--rows3", "1000", "--config-steps", "2",
-                             "--no-cpu-baseline", "--latency-qps", "0"])
+                             "--no-cpu-baseline", "--latency-qps", "0",
+                             "--host-rows-configs", "1000"])
     engines = []
 
     def make(forest):
@@ -97,6 +103,11 @@ def test_bench_rank_path_two_ranks():
     c3 = line["c3"]
     assert c3["rows"] == 1000 and c3["rows_per_gpu"] == 500 and c3["scaling"] == "strong"
     assert c3["ms_per_step"] >= 20.0
+    # the plugins' host-buffer path for the config
+    # workloads, on rank 0 (the stand-in's host predict)
+    hp = line["host_pipeline_c3"]
+    assert hp["rows"] == 1000 and hp["input_GBps"] > 0 and hp["dtype"] == "float32"
+    assert hp["bytes_per_row_in"] == 400
     rf = line["roofline"]
     assert rf["bound"] == "valu_issue" and rf["unit"] == "Ginst/s"
     assert 0 < rf["hbm_compulsory_frac"] < 1
@@ -114,7 +125,7 @@ def test_bench_cli_gpus_n_starts_n_ranks():
            "--engine", "tests.bench_stub:make", "--steps", "5", "--warmup", "1",
            "--rows", "2048", "--configs", "c3", "--rows3", "2000", "--config-steps", "1",
            "--cpu-seconds", "0.2", "--latency-qps", "200", "--latency-seconds", "0.5",
-           "--nan-variant", "0", "--host-rows", "0"]
+           "--nan-variant", "0", "--host-rows", "0", "--host-rows-configs", "0"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
