@@ -74,9 +74,9 @@ LAYOUT_KERNELS = {0: "heap_predict_kernel", 1: "explicit_predict_kernel",
 WALK_KERNELS = {0: "bheap_predict_kernel", 1: "bheap_fix_kernel", 2: "bheap_fix_kernel"}
 # the committed PMC pass each workload's roofline is priced on
 # (scripts/kernel_pmc.sh -> scripts/make_pmc_json.py)
-PMC_PASSES = {"c2": "profiles/r4c_c2_pmc.json", "c3": "profiles/r5i_c3_t16_pmc.json",
-              "c3_f64": "profiles/r5o_c3_f64_t16_pmc.json", "c3_maxbin": "profiles/r4d_c3_maxbin_pmc.json",
-              "c4": "profiles/r4c_c4_pmc.json", "c2_hist": "profiles/r4c_c2_hist_pmc.json"}
+PMC_PASSES = {"c2": "profiles/r6c_c2_pmc.json", "c3": "profiles/r6c_c3_pmc.json",
+              "c3_f64": "profiles/r6c_c3_f64_pmc.json", "c3_maxbin": "profiles/r6c_c3_maxbin_pmc.json",
+              "c4": "profiles/r6c_c4_pmc.json", "c2_hist": "profiles/r6c_c2_hist_pmc.json"}
 
 
 def pmc_path(key: str) -> str:
@@ -89,7 +89,8 @@ def launched_kernel(info: dict) -> str:
     if layout == 3:
         return WALK_KERNELS.get(info.get("walk"), "bheap_predict_kernel")
     if layout == 9:
-        return {1: "t8explicit_predict_kernel", 2: "t16explicit_predict_kernel"}.get(
+        return {1: "t8explicit_predict_kernel", 2: "t16explicit_predict_kernel",
+                3: "t16split_predict_kernel"}.get(
             info.get("bottom"), "texplicit_predict_kernel")
     return LAYOUT_KERNELS.get(layout, f"layout{layout}")
 

@@ -170,7 +170,9 @@ typedef struct ti_forest_info {
   int32_t tree_ilp;           /* record layouts: trees walked at once per lane       */
   int32_t n_stages;           /* staged layouts (7, 9): LDS stages of the forest     */
   int32_t top_depth;          /* layouts 8, 9: levels of each tree's heap top        */
-  int32_t bottom;             /* layout 9: 0 records, 1 compact u8 nodes (plan_tx8)  */
+  int32_t bottom;             /* layout 9: 0 records, 1 compact u8 nodes (plan_tx8),
+                                 2 compact u16 nodes, 3 compact u16 nodes walked two
+                                 lanes a row (round 6)                              */
   /* ABI 4: the TreeSHAP coefficient table of device slot 0 */
   int32_t shap_table;         /* 1 built, 0 not (yet) built, -1 not buildable: over
                                  TI_OPT_SHAP_TABLE_MB or its allocation failed; the

@@ -653,7 +653,8 @@ struct ti_forest {
   std::vector<uint32_t> h_tx_off, h_tx_nint;
   // layout 9's compact u8 bottom (plan_tx8): per tree the first bottom
   // position [T+1], and per bottom position the leaf value (ACC) / ordinal
-  int32_t tx8 = 0;                 // 1: compact u8 bottom, 2: compact u16 bottom
+  int32_t tx8 = 0;                 // 1: compact u8 bottom, 2: compact u16 bottom, 3: the u16
+                                   //   bottom walked two lanes a row (t16split_predict_kernel)
   uint32_t tx16_mask = 0;          //   u16: the bottom word's bin-offset bits (KArgs bin_mask)
   std::vector<uint32_t> h_tx8_pos;
   std::vector<unsigned char> h_tx8_val;
@@ -1739,10 +1740,16 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
   // 4.70 ms, 7 5.29, 8 5.72 (profiles/r3_tx8_sweep.jsonl)
   const int force_ilp = env_int("TI_LX_ILP", 0);
   int ilp = force_ilp > 0 ? (force_ilp >= 8 ? 8 : force_ilp == 7 ? 7 : 4) : 4;
+  // round 6: the u16 bottom two lanes a row when the tile's
+  // 2R threads fit a workgroup of 512 and leaves are scalars (the lower lane
+  // adds both halves' values in tree order); a group is 8 trees, 4 a lane.
+  // TI_TX16_SPLIT=0 (developer knob) keeps the one-lane walk.
+  const bool split = b16 && 2 * f->rx[0].rows <= 512 && d->leaf_width == 1 &&
+                     env_int("TI_TX16_SPLIT", 1) != 0;
   if (b16) {   // the u16 kernel is instantiated at 4 and 8 trees a lane
     // (C3 at 1M rows, profiles/r5f_c3_t16_sweep.jsonl: 8 trees a lane and a
     // top of 8 levels 5.25-5.28 ms; 12 or 16 a lane 5.37-10.9 ms)
-    ilp = env_int("TI_TX16_ILP", 8) >= 8 ? 8 : 4;
+    ilp = split ? 8 : env_int("TI_TX16_ILP", 8) >= 8 ? 8 : 4;
   }
   std::vector<int32_t> stages(1, 0);
   int t0 = 0;
@@ -1838,7 +1845,7 @@ bool plan_tx8(const ti_forest_desc* d, ti_forest* f, const std::vector<uint32_t>
   f->lx_stage_cap = static_cast<int64_t>(cap);
   f->lx_ilp = ilp;
   f->hx_top = D0;
-  f->tx8 = b16 ? 2 : 1;
+  f->tx8 = split ? 3 : b16 ? 2 : 1;
   f->tx16_mask = bmask16;
   f->layout = 9;
   return true;
@@ -2129,6 +2136,13 @@ KernelFn select_t16explicit(int xdt, int accum, int K, bool z, int ilp) {   // l
   if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(12, K, true, z, true, ilp);
   if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(12, K, true, z, true, ilp);
   return ti::kernels_df(12, K, true, z, true, ilp);
+}
+
+KernelFn select_t16split(int xdt, int accum, int K, bool z) {   // layout 9, u16, two lanes a row
+  if (xdt == TI_F32 && accum == TI_F32) return ti::kernels_ff(13, K, true, z, true, 4);
+  if (xdt == TI_F32 && accum == TI_F64) return ti::kernels_fd(13, K, true, z, true, 4);
+  if (xdt == TI_F64 && accum == TI_F64) return ti::kernels_dd(13, K, true, z, true, 4);
+  return ti::kernels_df(13, K, true, z, true, 4);
 }
 
 KernelFn select_hexplicit(int xdt, int accum, int K, bool z, int ilp) {
@@ -2423,15 +2437,18 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     a.tx_vals = d.tx8_val;
     a.tx_ord = d.tx8_ord;
     a.bin_mask = f->tx16_mask;
-    KernelFn fn = f->tx8 == 2 ? select_t16explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
+    KernelFn fn = f->tx8 == 3 ? select_t16split(xdt, f->accum, f->K, f->zero_rule != 0)
+                : f->tx8 == 2 ? select_t16explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
                 : f->tx8 ? select_t8explicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp)
                          : select_texplicit(xdt, f->accum, f->K, f->zero_rule != 0, f->lx_ilp, rx.b8 != 0);
     int rc = ensure_lds_attr(d.device, fn);
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    occ_note(fn, R, lds);
-  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
+    const int block = f->tx8 == 3 ? 2 * R : R;   // two lanes a row: 2R threads
+    if (block > 512) return fail(TI_ERR_UNSUPPORTED, "two-lane walk needs tiles of <= 256 rows");
+    occ_note(fn, block, lds);
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(block), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
   } else if (f->layout == 8) {

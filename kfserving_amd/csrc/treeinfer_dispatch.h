@@ -13,7 +13,7 @@ using KernelFn = void (*)(KArgs);
 // record explicit, 8 heap top + record bottom, 9 heap top + staged record
 // bottom (2, 4 and 5 were retired in round 3); 10 selects the fixed-layout
 // walk of layout 3 (bheap_fix_kernel), 11 layout 9's compact u8 bottom, 12
-// its compact u16 bottom.
+// its compact u16 bottom, 13 the u16 bottom walked two lanes a row.
 // fl: feature image in
 // LDS; z: LightGBM zero rule; b16 / pf: binned heap (and layout 9) bin width
 // and prefetch depth.
@@ -40,6 +40,12 @@ KernelFn select_layout(int layout, bool fl, bool z, bool b16, int pf) {
     return pf >= 8 ? t8explicit_predict_kernel<XT, ACC, KMAX, false, 8>
            : pf == 7 ? t8explicit_predict_kernel<XT, ACC, KMAX, false, 7>
                      : t8explicit_predict_kernel<XT, ACC, KMAX, false, 4>;
+  }
+  if (layout == 13) {   // the compact u16 bottom, two lanes a row: 4 trees a lane (8 a group)
+    if constexpr (sizeof(ACC) == 8) {
+      if (z) return t16split_predict_kernel<XT, ACC, KMAX, true, 4>;
+    }
+    return t16split_predict_kernel<XT, ACC, KMAX, false, 4>;
   }
   if (layout == 12) {   // layout 9 with the compact u16 bottom; pf carries the tree ILP
     if constexpr (sizeof(ACC) == 8) {

@@ -1337,17 +1337,21 @@ __device__ __forceinline__ void rx_bin_group(const KArgs& a, const XT (&x)[Q], i
 // lines: C3's 400-byte rows made that 0.57 ms of a 5.5 ms kernel).  Returns
 // (uniformly) whether the tile needs the slow step: a NaN, or with ZB an
 // exact 0.
+// NT threads bin the R-row tile (NT = R, or 2R for the two-lanes-a-row walk:
+// thread tid takes row tid mod R and every (NT / R)-th group of Q features).
 template <typename XT, bool ZB, bool KARY = false, bool SROOT = false, bool B8 = false>
 __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp, const KArgs& a,
-                                                   int64_t row0, int R, int tid) {
+                                                   int64_t row0, int R, int tid_in, int NT) {
   constexpr int Q = TI_RX_BINQ;
   const int F = a.n_features;
   const int FC = F < a.n_cols ? F : a.n_cols;
+  const int tid = tid_in & (R - 1);          // the row this thread bins (R: a power of two)
+  const int H = NT / R, h = tid_in / R;      // feature groups h, h + H, h + 2H, ...
   const int64_t row = row0 + tid;
   const bool live = row < a.n_rows;
   const XT* X = static_cast<const XT*>(a.X);
   bool has_nan = false;
-  if (tid == 0) *flag = 0;
+  if (tid_in == 0) *flag = 0;
   constexpr int V = 16 / sizeof(XT);   // elements per 16-byte load
   const bool tiled = temp != nullptr && a.bin_chunk >= Q && FC == F && (F % V) == 0 &&
                      ((reinterpret_cast<uintptr_t>(X) | (uintptr_t)(a.row_stride * sizeof(XT))) & 15) == 0;
@@ -1359,7 +1363,7 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
       const int kc = (F - f0) < a.bin_chunk ? (F - f0) : a.bin_chunk;
       const uint32_t kv = (uint32_t)kc / V;
       __syncthreads();   // temp is free: the previous chunk is searched
-      for (uint32_t e = tid; e < rows_here * kv; e += R) {
+      for (uint32_t e = tid_in; e < rows_here * kv; e += NT) {
         const uint32_t r = e / kv;
         const uint32_t cv = e - r * kv;
         const xv_t v = *reinterpret_cast<const xv_t*>(X + (row0 + r) * a.row_stride + f0 + cv * V);
@@ -1367,7 +1371,7 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
         for (int j = 0; j < V; ++j) temp[(cv * V + j) * R + r] = zero_map(v[j], a.lgb_zero_map);
       }
       __syncthreads();
-      for (int c = 0; c < kc; c += Q) {
+      for (int c = h * Q; c < kc; c += Q * H) {
         XT x[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) x[q] = c + q < kc ? temp[(c + q) * R + tid] : nan_value<XT>();
@@ -1376,7 +1380,7 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
     }
   } else {
     const XT* xr = X + (live ? row : a.n_rows - 1) * a.row_stride;
-    for (int f0 = 0; f0 < F; f0 += Q) {
+    for (int f0 = h * Q; f0 < F; f0 += Q * H) {
       XT x[Q];
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
@@ -1398,11 +1402,13 @@ __device__ __forceinline__ bool rx_stage_bins_impl(volatile int* flag, XT* temp,
 // layout 9 it cost C3 0.7 %, profiles/r2_kary_root_sweep.jsonl)
 template <typename XT, bool ZB, bool SROOT = false, bool B8 = false>
 __device__ __forceinline__ bool rx_stage_bins(volatile int* flag, const KArgs& a, int64_t row0,
-                                              int R, int tid, void* temp = nullptr) {
+                                              int R, int tid, void* temp = nullptr, int NT = 0) {
+  if (NT <= 0) NT = R;
   if (a.bin_kary > 0)
     return rx_stage_bins_impl<XT, ZB, true, SROOT, B8>(flag, static_cast<XT*>(temp), a, row0, R,
-                                                       tid);
-  return rx_stage_bins_impl<XT, ZB, false, false, B8>(flag, static_cast<XT*>(temp), a, row0, R, tid);
+                                                       tid, NT);
+  return rx_stage_bins_impl<XT, ZB, false, false, B8>(flag, static_cast<XT*>(temp), a, row0, R, tid,
+                                                      NT);
 }
 
 // Per step every tree's bin read is issued first, then each tree's decision
@@ -2159,25 +2165,71 @@ __device__ __forceinline__ bool t16_right_slow(uint32_t x, uint32_t b, bool zf) 
   return right;
 }
 
-template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP>
+// The two-lanes-a-row walk (t16split_predict_kernel): a lane's partner
+// (lane l + 32 for l < 32) holds the same row and walks the other half of
+// each group of 2 x ILP trees.  v_permlane32_swap hands the lower half the
+// upper half's values (ISA: vdst lanes 32-63 <-> vsrc lanes 0-31; the
+// builtin returns {vdst, vsrc}, so lane l < 32 finds lane l + 32's value in
+// the second); the upper half gets its own back and its sums are never used.
+__device__ __forceinline__ uint32_t from_upper_half(uint32_t v) {
+  return __builtin_amdgcn_permlane32_swap(v, v, false, false)[1];
+}
+template <typename ACC>
+__device__ __forceinline__ ACC from_upper_half(ACC v) {
+  if constexpr (sizeof(ACC) == 8) {
+    const double d = static_cast<double>(v);
+    const uint32_t lo = from_upper_half((uint32_t)__double2loint(d));
+    const uint32_t hi = from_upper_half((uint32_t)__double2hiint(d));
+    return static_cast<ACC>(__hiloint2double((int)hi, (int)lo));
+  } else {
+    return static_cast<ACC>(__uint_as_float(from_upper_half(__float_as_uint(static_cast<float>(v)))));
+  }
+}
+
+// A split group's leaves in the library's order: the lower lane's own trees
+// j .. j + ILP - 1, then its partner's j + ILP .. j + 2 ILP - 1.  The swaps
+// run on all 64 lanes before any lane branches.
+template <typename ACC, int KMAX, int ILP>
+__device__ __forceinline__ void t16_flush_split(const KArgs& a, ACC (&acc)[KMAX],
+                                                const ACC (&pend)[ILP], const int (&pend_t)[ILP]) {
+  ACC pp[ILP];
+  int pt[ILP];
+#pragma unroll
+  for (int q = 0; q < ILP; ++q) {
+    pp[q] = from_upper_half<ACC>(pend[q]);
+    pt[q] = (int)from_upper_half((uint32_t)pend_t[q]);
+  }
+  t8_flush<ACC, KMAX, ILP>(a, acc, pend, pend_t);
+  t8_flush<ACC, KMAX, ILP>(a, acc, pp, pt);
+}
+
+template <typename ACC, int KMAX, bool ZERO, bool SLOW, bool VIS, int ILP, bool SPLIT = false>
 __device__ __forceinline__ void t16_stage(const KArgs& a, ACC (&acc)[KMAX], int t0, int t1,
                                           uint32_t sbase, uint32_t lane_off, int64_t row,
-                                          bool live, ACC (&pend)[ILP], int (&pend_t)[ILP]) {
+                                          bool live, ACC (&pend)[ILP], int (&pend_t)[ILP],
+                                          int half = 0) {
   rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
   rx_cu32* tx_pos = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.tx_pos));
   const int D0 = a.depth;
   const uint32_t topb = 8u << D0;                   // 2^(D0+1) u32
   const uint32_t zfb = ZERO ? kT16ZfBytes : 0u;     // zero-flip bits before the bottom
   const uint32_t bmask = a.bin_mask;                // word index | half (the lane part cleared)
-  for (int j = t0; j < t1; j += ILP) {
-    uint32_t base[ILP], idx[ILP], nd[ILP];
+  for (int jg = t0; jg < t1; jg += (SPLIT ? 2 : 1) * ILP) {
+    const int j = SPLIT ? jg + half * ILP : jg;   // this lane's first tree of the group
+    uint32_t base[ILP], idx[ILP], nd[ILP], pos0[ILP];
 #pragma unroll
     for (int q = 0; q < ILP; ++q) {
-      const int tq = (j + q) < t1 ? (j + q) : (t1 - 1);
-      base[q] = sbase + tx_off[tq];
+      // both halves' tree tables by wave-uniform indices (scalar loads), then
+      // the lane's half selected: a lane-dependent index would make every
+      // table read a vector gather
+      const int ta = (jg + q) < t1 ? (jg + q) : (t1 - 1);
+      const int tb = SPLIT ? ((jg + ILP + q) < t1 ? (jg + ILP + q) : (t1 - 1)) : ta;
+      const uint32_t oa = tx_off[ta], ob = tx_off[tb];
+      base[q] = sbase + (SPLIT && half ? ob : oa);
+      if (SPLIT) pos0[q] = half ? tx_pos[tb] : tx_pos[ta];
       idx[q] = 1u;
       nd[q] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
-          static_cast<uintptr_t>(base[q] + 4u));   // the root: one broadcast read
+          static_cast<uintptr_t>(base[q] + 4u));   // the root: one broadcast read per half
     }
     for (int l = 0; l < D0; ++l) {   // the top, as layout 9's (record x words)
       uint32_t b[ILP];
@@ -2243,10 +2295,13 @@ __device__ __forceinline__ void t16_stage(const KArgs& a, ACC (&acc)[KMAX], int 
 #pragma unroll
     for (int q = 0; q < ILP; ++q) {
       const int tq = (j + q) < t1 ? (j + q) : (t1 - 1);
-      li[q] = tx_pos[tq] + ((x[q] >> 1) & 0x1FEu) + ((x[q] >> 16) == 0u ? 1u : 0u);
+      li[q] = (SPLIT ? pos0[q] : tx_pos[tq]) + ((x[q] >> 1) & 0x1FEu) +
+              ((x[q] >> 16) == 0u ? 1u : 0u);
     }
     if (VIS) {
-      t8_flush<ACC, KMAX, ILP>(a, acc, pend, pend_t);   // the previous group's leaves
+      // the previous group's leaves
+      if (SPLIT) t16_flush_split<ACC, KMAX, ILP>(a, acc, pend, pend_t);
+      else t8_flush<ACC, KMAX, ILP>(a, acc, pend, pend_t);
 #pragma unroll
       for (int q = 0; q < ILP; ++q) {
         pend[q] = static_cast<const ACC*>(a.tx_vals)[li[q]];
@@ -2260,7 +2315,7 @@ __device__ __forceinline__ void t16_stage(const KArgs& a, ACC (&acc)[KMAX], int 
           const int64_t lf = a.leaf_base[t] + (int64_t)a.tx_ord[li[q]];
           if (a.kind == TI_OUTPUT_LEAF) {
             if (live) static_cast<int32_t*>(a.out)[row * a.n_trees + t] = a.exp_leaf_ids[lf];
-          } else {
+          } else if (!SPLIT) {   // (the host gives the split walk scalar leaves only)
             add_leaf<ACC, KMAX>(acc, static_cast<const ACC*>(a.leaves) + lf * a.leaf_width, 0,
                                 a.leaf_width, a.tree_group[t]);
           }
@@ -2320,6 +2375,75 @@ __global__ void __launch_bounds__(512) t16explicit_predict_kernel(const KArgs a)
   }
   if (vis) t8_flush<ACC, KMAX, ILP>(a, acc, pend, pend_t);
   if (!live || a.kind == TI_OUTPUT_LEAF) return;
+  finish_row<ACC, KMAX>(acc, a, row);
+}
+
+// Two lanes a row (round 6): the R-row tile of the u16 compact
+// walk on 2R threads.  Wave w holds rows 32w .. 32w + 31 twice: lanes 0-31
+// walk the first ILP trees of every group of 2 ILP, lanes 32-63 the other
+// ILP, so a CU keeps twice the waves resident with the same LDS (bins,
+// stage); each 32-lane half is one LDS lane group and reads 32 distinct
+// rows' bins, conflict-free as the one-lane walk.  The lower lane adds the
+// group's leaves in tree order (t16_flush_split) and writes the row.
+template <typename XT, typename ACC, int KMAX, bool ZERO, int ILP>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) t16split_predict_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int PF = 4;   // 2R threads prefetch a stage of at most kLxPf x 16 B x R
+  const int NT = blockDim.x;
+  const int R = NT >> 1;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int half = lane >> 5;
+  const int rloc = ((tid >> 6) << 5) | (lane & 31);   // the tile row of this lane pair
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t row = row0 + rloc;
+  const bool live = row < a.n_rows;
+  volatile int* flag = reinterpret_cast<volatile int*>(smem + (size_t)a.bin_words * R * 4);
+  u32x4* stage = reinterpret_cast<u32x4*>(smem + a.stage_off);
+  const uint32_t lane_off = (uint32_t)rloc * 4u;
+  rx_cu32* tx_off = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.rx_base));
+  rx_cu32* sst = reinterpret_cast<rx_cu32*>(reinterpret_cast<uintptr_t>(a.stage_start));
+  const unsigned char* img = a.trees;
+  const int NS = a.n_stages;
+  auto lo_of = [&](int s) { return tx_off[sst[s]]; };   // trees start 16-byte aligned
+  auto n16_of = [&](int s) { return (int)((tx_off[sst[s + 1]] - tx_off[sst[s]]) >> 4); };
+  // the first stage is fetched after the binning, not during it: the float64
+  // binning's 5-ary search keeps 8 x 4 doubles in flight, and prefetch
+  // registers live across it took the kernel past the 128 VGPRs 4 waves a
+  // SIMD allow (138: 3 waves, one workgroup a CU); the exposed fetch is one
+  // per tile, ~0.3 % of it
+  const bool slow = rx_stage_bins<XT, ZERO, false, false>(flag, a, row0, R, tid, stage, NT);
+  u32x4 pf[PF];
+  prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(0)), n16_of(0), tid, NT);
+  const bool vis = a.leaf_width == 1 && a.kind != TI_OUTPUT_LEAF;
+  ACC acc[KMAX];
+  init_acc(acc, a);
+  ACC pend[ILP];   // the previous group's leaf values (this lane's half)
+  int pend_t[ILP];
+#pragma unroll
+  for (int q = 0; q < ILP; ++q) {
+    pend[q] = ACC(0);
+    pend_t[q] = -1;
+  }
+  for (int s = 0; s < NS; ++s) {
+    const int t0 = (int)sst[s], t1 = (int)sst[s + 1];
+    const uint32_t lo = lo_of(s);
+    __syncthreads();   // the previous stage's walk is over
+    commit_u<PF>(pf, stage, n16_of(s), tid, NT);
+    __syncthreads();
+    const int sn = s + 1 < NS ? s + 1 : s;
+    prefetch_u<PF>(pf, reinterpret_cast<const u32x4*>(img + lo_of(sn)), n16_of(sn), tid, NT);
+    const uint32_t sbase = (uint32_t)a.stage_off - lo;   // LDS address = sbase + image byte
+    if (slow) {
+      if (vis) t16_stage<ACC, KMAX, ZERO, true, true, ILP, true>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t, half);
+      else t16_stage<ACC, KMAX, ZERO, true, false, ILP, true>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t, half);
+    } else {
+      if (vis) t16_stage<ACC, KMAX, ZERO, false, true, ILP, true>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t, half);
+      else t16_stage<ACC, KMAX, ZERO, false, false, ILP, true>(a, acc, t0, t1, sbase, lane_off, row, live, pend, pend_t, half);
+    }
+  }
+  if (vis) t16_flush_split<ACC, KMAX, ILP>(a, acc, pend, pend_t);
+  if (!live || a.kind == TI_OUTPUT_LEAF || half) return;
   finish_row<ACC, KMAX>(acc, a, row);
 }
 

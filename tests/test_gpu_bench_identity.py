@@ -51,3 +51,48 @@ def test_headline_two_streams_same_outputs():
     assert ss["kernel_ms"] > 0 and ss["ms_per_step"] > 0
     assert abs(line["value"] - 262144 * 6 / (line["ms_per_step"] * 6e-3)) < 1e-6 * line["value"]
     assert line["roofline"]["kernel_ms"] == ss["kernel_ms"]
+
+
+@pytest.mark.parametrize("key", ["c2", "c2_hist", "c3", "c3_f64", "c3_maxbin", "c4"])
+def test_pmc_pass_duration_matches_this_box(key):
+    """a committed PMC pass prices the launch bench.py
+    times only if its profiled kernel duration (the pass's own
+    --kernel-trace) is within 10 % of the same kernel timed here with HIP
+    events on its launch stream, on the same 1M-row workload as
+    scripts/kernel_workload.py (its forest, dtype and seed)."""
+    import sys
+    import torch
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "scripts"))
+    import kernel_workload as kw
+    from kfserving_amd.engine import DeviceForest
+    from kfserving_amd.forest import OUT_PREDICT, TI_F32, TI_F64
+    forest, F, dtype = kw.forest_of(key)
+    pmc = bench.load_pmc(bench.pmc_path(key))
+    rows = int(pmc["rows"])
+    dev = DeviceForest(forest, [0])
+    try:
+        assert bench.pmc_mismatch(pmc, key, rows, dev.info()) is None
+        X = bench.device_normal(rows, F, 3, "cuda:0", dtype)
+        out = torch.empty(rows * forest.output_width(OUT_PREDICT),
+                          dtype=torch.float64 if forest.accum_dtype else torch.float32,
+                          device="cuda")
+        xdt = TI_F64 if dtype == "float64" else TI_F32
+        st = torch.cuda.current_stream()
+
+        def step():
+            dev.predict_device(X.data_ptr(), xdt, rows, F, F, OUT_PREDICT, out.data_ptr(),
+                               out.numel(), stream=st.cuda_stream)
+        step()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            step()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 5
+    finally:
+        dev.close()
+    prof_ms = pmc["profiled_kernel_ns"] / 1e6
+    assert abs(ms - prof_ms) <= 0.10 * prof_ms, (key, ms, prof_ms)
