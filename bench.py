@@ -74,8 +74,8 @@ LAYOUT_KERNELS = {0: "heap_predict_kernel", 1: "explicit_predict_kernel",
 WALK_KERNELS = {0: "bheap_predict_kernel", 1: "bheap_fix_kernel", 2: "bheap_fix_kernel"}
 # the committed PMC pass each workload's roofline is priced on
 # (scripts/kernel_pmc.sh -> scripts/make_pmc_json.py)
-PMC_PASSES = {"c2": "profiles/r6c_c2_pmc.json", "c3": "profiles/r6c_c3_pmc.json",
-              "c3_f64": "profiles/r6c_c3_f64_pmc.json", "c3_maxbin": "profiles/r6c_c3_maxbin_pmc.json",
+PMC_PASSES = {"c2": "profiles/r6c_c2_pmc.json", "c3": "profiles/r6g_c3_pmc.json",
+              "c3_f64": "profiles/r6g_c3_f64_pmc.json", "c3_maxbin": "profiles/r6c_c3_maxbin_pmc.json",
               "c4": "profiles/r6c_c4_pmc.json", "c2_hist": "profiles/r6c_c2_hist_pmc.json"}
 
 

@@ -2226,7 +2226,10 @@ __device__ __forceinline__ void t16_stage(const KArgs& a, ACC (&acc)[KMAX], int 
       const int tb = SPLIT ? ((jg + ILP + q) < t1 ? (jg + ILP + q) : (t1 - 1)) : ta;
       const uint32_t oa = tx_off[ta], ob = tx_off[tb];
       base[q] = sbase + (SPLIT && half ? ob : oa);
-      if (SPLIT) pos0[q] = half ? tx_pos[tb] : tx_pos[ta];
+      if constexpr (SPLIT) {   // both loaded (scalar), then selected: a select of two
+        const uint32_t pa = tx_pos[ta], pb = tx_pos[tb];   // loads became one gather
+        pos0[q] = half ? pb : pa;
+      }
       idx[q] = 1u;
       nd[q] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
           static_cast<uintptr_t>(base[q] + 4u));   // the root: one broadcast read per half

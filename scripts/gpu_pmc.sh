@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for w in "$@"; do
   case $w in
     c2|c2_hist) k=bheap_fix_kernel; lay=bheap; extra="--walk-id 2 --walk-step fixed-layout-walk,scalar-root --model-bytes 2800000" ;;
-    c3|c3_f64) k=t16explicit_predict_kernel; lay=texplicit; extra="" ;;
+    c3|c3_f64) k=t16split_predict_kernel; lay=texplicit; extra="" ;;
     c3_maxbin) k=t8explicit_predict_kernel; lay=texplicit; extra="" ;;
     c4) k=hexplicit_predict_kernel; lay=hexplicit; extra="" ;;
   esac

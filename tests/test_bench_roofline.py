@@ -40,8 +40,8 @@ def test_c2_roofline_mismatch_says_why(info, why):
 
 
 @pytest.mark.parametrize("key,info,bound", [
-    ("c3", {"layout": 9, "bottom": 2}, "td_busy"),
-    ("c3_f64", {"layout": 9, "bottom": 2}, "td_busy"),
+    ("c3", {"layout": 9, "bottom": 3}, "td_busy"),
+    ("c3_f64", {"layout": 9, "bottom": 3}, "td_busy"),
     ("c3_maxbin", {"layout": 9, "bottom": 1}, "lds_array"),
     ("c4", {"layout": 8}, "td_busy"),
 ])
