@@ -711,7 +711,7 @@ def c5_http_leg(args, world, protocol="v1", device="cuda"):
     except Exception as e:   # reported, not fatal: the headline stands without it
         return {"error": str(e)[-500:]}
     keep = ("offered_qps", "req_per_s", "rows_per_s", "p50_ms", "p90_ms", "p99_ms", "max_ms",
-            "requests", "lost", "non200", "conn_errors")
+            "requests", "lost", "non200", "conn_errors", "conns")
     res = {"devices": world, "workers": world, "io_threads_per_worker": io,
            "conns": conns, "conns_per_gpu": args.c5_conns_per_gpu,
            "loadgen_threads": lg_threads, "rows_per_request": "U{1..64}",
