@@ -1,5 +1,7 @@
 # one GPU call of the round: the GPU test suite, the bench, then PMC passes of
-# the named workloads.  A failing test does not stop the call; a crash, abort
+# the named workloads, then the headline alone (one stream, no other legs)
+# under rocprofv3 --kernel-trace --stats, whose average the line's kernel_ms
+# must match.  A failing test does not stop the call; a crash, abort
 # or time limit does.  Usage: bash scripts/gpu_round.sh PREFIX [pmc workloads...]
 set -o pipefail
 mkdir -p gpurun_out
@@ -10,4 +12,4 @@ rc=$?; echo "tests rc=$rc"; fatal $rc tests
 timeout -k 10 300 python bench.py > gpurun_out/${P}_bench.jsonl 2> gpurun_out/${P}_bench.err || exit 2
 [ $# -gt 0 ] && { bash scripts/gpu_pmc.sh $P "$@" || exit 3; }
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${P}_prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 5 --configs "" --no-cpu-baseline --latency-qps 0 --host-rows 0 > $GRAFT_REPO_ROOT/gpurun_out/${P}_bench_prof.jsonl 2>&1 || exit 5
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${P}_prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 5 --configs "" --no-cpu-baseline --latency-qps 0 --host-rows 0 --host-rows-configs 0 --nan-variant 0 --no-tree-shard --streams 1 --c5-http-qps "" --c5-http-v2-qps "" > $GRAFT_REPO_ROOT/gpurun_out/${P}_bench_prof.jsonl 2>&1 || exit 5
