@@ -12,7 +12,7 @@ Also reported (rank 0):
   roofline     -- the resource that binds the C2 kernel:
                   the busiest of VALU issue, the LDS array and the TD in the
                   committed rocprofv3 PMC pass of the same kernel
-                  (profiles/r4c_c2_pmc.json), priced on that pass's own cycles
+                  (profiles/r6c_c2_pmc.json), priced on that pass's own cycles
                   (GRBM_GUI_ACTIVE per XCD): the LDS array, ~0.67.  `valu`
                   keeps the VALU view: achieved = VALU wave-instructions per
                   launch / the kernel's average duration from HIP events on
