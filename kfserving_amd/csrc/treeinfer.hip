@@ -535,10 +535,6 @@ constexpr uint32_t kPadMeta = ti::kMetaNanLeft;
 struct DeviceForest {
   int device = -1;
   hipStream_t stream = nullptr;
-  // rows one launch round of the predict kernel covers (tile rows x resident
-  // workgroups a CU x CUs), per input type, noted at the first launch: host
-  // batches are chunked in whole rounds (chunk_rows_for)
-  int64_t round_rows[2] = {0, 0};
   // heap layout: one record per tree, float32-input and float64-input flavours
   unsigned char* heap32 = nullptr;
   unsigned char* heap64 = nullptr;
@@ -2177,24 +2173,10 @@ int ensure_lds_attr(int device, KernelFn fn) {
   return TI_OK;
 }
 
-// At the first launch of a replica (per input type) note the rows one launch
-// round covers: the runtime's occupancy calculator's workgroups a CU for this
-// launch shape x the CUs x the workgroup's tile rows.  TI_OCC=1 (developer
-// knob) also prints, once per kernel, that occupancy (a diagnostic for the PMC
-// passes' resident-wave counts).
-void occ_note(DeviceForest& d, int xdt, KernelFn fn, int block, size_t lds, int tile_rows = 0) {
-  const int ii = xdt == TI_F64 ? 1 : 0;
-  if (d.round_rows[ii] == 0) {
-    int n = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), block,
-                                                     lds) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device) != hipSuccess) {
-      (void)hipGetLastError();
-      n = cus = 0;
-    }
-    d.round_rows[ii] = n > 0 && cus > 0 ? static_cast<int64_t>(n) * cus * (tile_rows > 0 ? tile_rows : block)
-                                        : -1;
-  }
+// TI_OCC=1: print, once per kernel, the workgroups per CU the runtime's
+// occupancy calculator allows for this launch shape (a diagnostic for the
+// PMC passes' resident-wave counts).
+void occ_note(KernelFn fn, int block, size_t lds) {
   static const int on = env_int("TI_OCC", 0);
   if (!on) return;
   static std::mutex mu;
@@ -2372,7 +2354,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    occ_note(d, xdt, fn, R, lds);
+    occ_note(fn, R, lds);
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
@@ -2396,7 +2378,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    occ_note(d, xdt, fn, R, lds);
+    occ_note(fn, R, lds);
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
@@ -2426,7 +2408,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    occ_note(d, xdt, fn, R, lds);
+    occ_note(fn, R, lds);
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
@@ -2465,7 +2447,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
     const int block = f->tx8 == 3 ? 2 * R : R;   // two lanes a row: 2R threads
     if (block > 512) return fail(TI_ERR_UNSUPPORTED, "two-lane walk needs tiles of <= 256 rows");
-    occ_note(d, xdt, fn, block, lds, R);
+    occ_note(fn, block, lds);
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(block), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
@@ -2497,7 +2479,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
     if (rc) return rc;
     const int64_t grid = (rows + R - 1) / R;
     if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-    occ_note(d, xdt, fn, R, lds);
+    occ_note(fn, R, lds);
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
     TI_HIP(hipGetLastError());
     return TI_OK;
@@ -2516,7 +2498,7 @@ int launch(ti_forest* f, DeviceForest& d, const void* X, int xdt, int64_t rows, 
   if (rc) return rc;
   const int64_t grid = (rows + R - 1) / R;
   if (grid > 0x7fffffff) return fail(TI_ERR_INVALID, "too many rows for one launch");
-  occ_note(d, xdt, fn, R, lds);
+  occ_note(fn, R, lds);
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(R), lds, stream, a);
   TI_HIP(hipGetLastError());
   return TI_OK;
@@ -2571,22 +2553,6 @@ int64_t chunk_rows(size_t row_bytes) {
   int64_t r = static_cast<int64_t>((static_cast<size_t>(std::max(mb, 1)) << 20) / std::max<size_t>(row_bytes, 1));
   r = std::max<int64_t>(512, r & ~int64_t(511));
   return r;
-}
-
-// Host-batch chunks in whole launch rounds of the replica's kernel (round 6):
-// a 64 MB chunk of C3 float32 rows is 1.28 rounds of its 256-row tiles on
-// 512 workgroup slots, so each chunk's kernel ran two rounds, one of them a
-// quarter full, and took longer than the chunk's H2D.  Rounded down to whole
-// rounds when at least one fits, up to one round when it is within 2x the
-// size; unchanged before the replica's first launch (round unknown).
-int64_t chunk_rows_for(const DeviceForest& d, int xdt, size_t row_bytes) {
-  int64_t ch = chunk_rows(row_bytes);
-  const int64_t r = d.round_rows[xdt == TI_F64 ? 1 : 0];
-  if (r > 0) {
-    if (ch >= r) ch = (ch / r) * r;
-    else if (2 * ch >= r) ch = r;
-  }
-  return ch;
 }
 
 // Batches larger than one chunk: chunks alternate between two lanes (streams
@@ -2767,7 +2733,7 @@ int predict_shard(ti_forest* f, int slot, DeviceForest& d, const unsigned char* 
   std::lock_guard<std::mutex> lk(d.mu);
   TI_HIP(hipSetDevice(d.device));
   {
-    const int64_t ch = chunk_rows_for(d, xdt, static_cast<size_t>(stride) * dtype_size(xdt));
+    const int64_t ch = chunk_rows(static_cast<size_t>(stride) * dtype_size(xdt));
     if (rows > ch) {
       if (reg) {
         const int rc = predict_registered(f, slot, d, X, xdt, rows, cols, stride, kind, out, ch,
