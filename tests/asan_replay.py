@@ -268,6 +268,27 @@ def main():
             st = first_status(resp)
             if c["expect"] and st not in c["expect"]:
                 fail(f"{c['name']}: status {st}, expected {c['expect']}: {resp[:120]!r}")
+        # the corpus again from 16 client threads at once (the IO threads,
+        # the batcher's completions and the application's answers interleave:
+        # a race that frees or reuses a connection's buffers early shows here)
+        import threading
+        small = [base64.b64decode(c["data"]) for c in cases if c["kind"] == "http"]
+        errs = []
+
+        def hammer(k):
+            rng_k = np.random.default_rng(1000 + k)
+            for _ in range(40):
+                data = small[int(rng_k.integers(0, len(small)))]
+                try:
+                    send(run.port, data, shut=True, timeout=10)
+                except OSError as e:   # a refused or reset connection is an answer too
+                    errs.append(str(e))
+        th = [threading.Thread(target=hammer, args=(k,)) for k in range(16)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        n_http += 16 * 40
         alive = send(run.port, b"GET /v1/models/%s HTTP/1.1\r\nHost: x\r\n\r\n" % MODEL.encode())
         if first_status(alive) != 200:
             fail(f"server not answering after the corpus: {alive[:120]!r}")
