@@ -33,6 +33,12 @@ def _rows(rng, n, F, dtype, frac):
     return X.astype(dtype)
 
 
+def _env(seed):
+    """Every other case forces a layout or a walk (developer knobs; the
+    conftest sets TI_DEV_KNOBS), so each kernel family meets random shapes."""
+    return FORCED[(seed // 2) % len(FORCED)] if seed % 2 == 1 else {}
+
+
 def _lgb_case(seed):
     rng = np.random.default_rng([seed, 61])
     T = int(rng.choice([1, 2, 3, 7, 9, 17, 40]))
@@ -40,6 +46,8 @@ def _lgb_case(seed):
     F = int(rng.choice([1, 3, 28, 100, 120]))
     K = int(rng.choice([1, 1, 3]))
     maxbin = bool(rng.integers(0, 2))
+    if "TI_TX16_SPLIT" in _env(seed):   # the one-lane u16 walk: i.i.d. thresholds
+        maxbin, leaves = False, 255
     mts = [(lf.MISSING_NONE,), (lf.MISSING_ZERO,), (lf.MISSING_NAN,),
            (lf.MISSING_NONE, lf.MISSING_ZERO, lf.MISSING_NAN)][int(rng.integers(0, 4))]
     if maxbin:
@@ -56,8 +64,6 @@ def _lgb_case(seed):
     return rng, trees, f, F, K, dict(T=T * K, leaves=leaves, F=F, K=K, maxbin=maxbin, mts=mts)
 
 
-# every third case also forces a layout or a walk (developer knobs; the
-# conftest sets TI_DEV_KNOBS), so each kernel family meets random shapes
 FORCED = [{}, {"TI_TX16_SPLIT": "0"}, {"TI_FORCE_LAYOUT": "lexplicit"},
           {"TI_FORCE_LAYOUT": "rexplicit"}, {"TI_FORCE_LAYOUT": "hexplicit"},
           {"TI_FORCE_LAYOUT": "explicit"}, {"TI_TX8": "0"}, {"TI_TX16": "0"}]
@@ -66,7 +72,7 @@ FORCED = [{}, {"TI_TX16_SPLIT": "0"}, {"TI_FORCE_LAYOUT": "lexplicit"},
 @pytest.mark.parametrize("seed", range(64))
 def test_fuzz_lightgbm_forests(seed, monkeypatch):
     rng, trees, f, F, K, desc = _lgb_case(seed)
-    env = FORCED[(seed // 3) % len(FORCED)] if seed % 3 == 2 else {}
+    env = _env(seed)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     desc["env"] = env
@@ -115,7 +121,7 @@ def test_fuzz_cases_reach_every_walk(monkeypatch):
     seen = set()
     for seed in range(64):
         _, _, f, _, _, _ = _lgb_case(seed)
-        env = FORCED[(seed // 3) % len(FORCED)] if seed % 3 == 2 else {}
+        env = _env(seed)
         with monkeypatch.context() as m:
             for k, v in env.items():
                 m.setenv(k, v)
