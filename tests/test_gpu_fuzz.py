@@ -131,3 +131,47 @@ def test_fuzz_cases_reach_every_walk(monkeypatch):
         seen.add((info["layout"], info["bottom"] if info["layout"] == 9 else -1))
     want = {(9, 3), (9, 2), (9, 1), (9, 0), (7, -1), (6, -1), (8, -1), (1, -1)}
     assert want <= seen, sorted(seen)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_sklearn_forests_vs_sklearn(seed, monkeypatch):
+    """Random sklearn forests fitted here (RandomForest / ExtraTrees,
+    regressor / classifier, depth 1 to unlimited, 1 to 20 estimators, 1 to 40
+    features), every other one on a forced layout, checked against sklearn
+    1.7.2's own predict / predict_proba / apply on rows with NaN (the trees'
+    missing_go_to_left)."""
+    from sklearn.ensemble import (ExtraTreesClassifier, ExtraTreesRegressor,
+                                  RandomForestClassifier, RandomForestRegressor)
+    from kfserving_amd.forest import OUT_PREDICT
+    from kfserving_amd.formats.sklearn_format import forest_from_sklearn
+    rng = np.random.default_rng([seed, 63])
+    F = int(rng.choice([1, 7, 40]))
+    n_est = int(rng.choice([1, 5, 20]))
+    depth = [1, 4, 12, None][int(rng.integers(0, 4))]
+    kind = int(rng.integers(0, 4))
+    Xt = rng.standard_normal((1500, F)).astype(np.float32)
+    if kind < 2:
+        y = Xt[:, 0] * 2 + np.sin(Xt[:, -1] * 3) + rng.normal(0, 0.3, 1500)
+        Est = RandomForestRegressor if kind == 0 else ExtraTreesRegressor
+    else:
+        y = (Xt[:, 0] + rng.normal(0, 0.5, 1500) > 0).astype(int) + (Xt[:, -1] > 1).astype(int)
+        Est = RandomForestClassifier if kind == 2 else ExtraTreesClassifier
+    est = Est(n_estimators=n_est, max_depth=depth, max_leaf_nodes=None if depth else 300,
+              random_state=seed, n_jobs=1).fit(Xt, y)
+    if seed % 2 == 1:
+        monkeypatch.setenv("TI_FORCE_LAYOUT", ["rexplicit", "lexplicit", "texplicit",
+                                               "explicit"][(seed // 2) % 4])
+    f = forest_from_sklearn(est)
+    dev = DeviceForest(f, [0])
+    try:
+        for n in (1, 257, 3001):
+            X = rng.standard_normal((n, F)).astype(np.float32)
+            X[rng.random(X.shape) < 0.02] = np.nan
+            if kind < 2:
+                assert np.array_equal(dev.predict(X, OUT_PREDICT), est.predict(X)), (seed, n)
+            else:
+                got = dev.predict(X, OUT_MARGIN).reshape(n, -1)
+                assert np.array_equal(got, est.predict_proba(X)), (seed, n)
+            assert np.array_equal(dev.predict(X, OUT_LEAF), est.apply(X)), (seed, n)
+    finally:
+        dev.close()
