@@ -45,6 +45,8 @@ def main():
     p.add_argument("--trees", type=int, default=0,
                    help="c2 / c2_hist / c3*: the first N trees (fixed cost vs per-tree cost; "
                         "C3's image against one XCD's 4 MB L2)")
+    p.add_argument("--tree-start", type=int, default=0,
+                   help="c4: the slice starts at this tree (with --trees: trees [start, start + N))")
     p.add_argument("--x-buffers", type=int, default=1,
                    help="copies of the batch the launches rotate through (bench.py uses 3 for C2)")
     p.add_argument("--streams", type=int, default=1,
@@ -65,6 +67,9 @@ def main():
         from kfserving_amd.formats import lightgbm_format as lf
         gen = lf.synthetic_maxbin_trees if a.workload == "c3_maxbin" else lf.synthetic_leafwise_trees
         forest = bench._lgb_forest(gen(1000, 255, 100, seed=1)[:a.trees], "first trees")[0]
+    elif (a.trees or a.tree_start) and a.workload == "c4":
+        t1 = a.tree_start + a.trees if a.trees else forest.n_trees
+        forest = forest.tree_subset(a.tree_start, t1, keep_base=True)
     dev = DeviceForest(forest, [0])
     Xs = [bench.device_normal(a.rows, F, 3, "cuda:0", dtype)]
     Xs += [Xs[0].clone() for _ in range(max(0, a.x_buffers - 1))]
